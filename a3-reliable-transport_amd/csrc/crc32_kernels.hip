@@ -1,0 +1,755 @@
+// crc32_kernels.hip — CDNA4 (gfx950) kernels for WTP's per-packet CRC-32.
+//
+// Reference path being replaced (mmheyer/a3-reliable-transport):
+//   crc32()  cpp/src/common/Crc32.hpp:91-102 — byte-at-a-time Sarwate loop, one call
+//            per DATA payload (Packet.cpp:13 sender build, Receiver.cpp:204 verify).
+//
+// Two kernel families, both HBM-read-bound integer work (no MFMA):
+//
+// 1. k_fixed_braid<ROWS> — equal-length payloads whose ends are 16-B aligned (the
+//    1456-B DATA chunk case).  16 lanes per packet, 4 packets per wave.  Each lane owns
+//    4 interleaved "braids" (CRC streams over every 64th dword of the packet), so the
+//    16 lanes of a packet read 256 contiguous bytes per row with global_load_dwordx4
+//    (fully coalesced, no LDS staging) and every lane carries 4 independent
+//    dependency chains.  Per dword: one v_perm_b32 builds each LDS address and one
+//    ds_read_b32 fetches the table word; the tables are replicated 32x in LDS so that
+//    lane L always hits bank L%32 (conflict-free random lookups).  At the end the 64
+//    braid registers of a packet are folded with x^(-32b) operators (in-lane, then a
+//    4-step cross-lane tree).
+//
+// 2. k_pieces<Prov, Epi> — anything else (mixed lengths, odd strides, unaligned
+//    buffers, receiver verify).  Each packet is cut into pieces of S = 64 bytes
+//    counted back from its end (the head piece is shorter); pieces of consecutive
+//    packets are packed densely into the 64 lanes of a wave ("wavefront-packed
+//    tails"), each lane runs a slice-by-4 chain over its piece (replicated tables),
+//    and a segmented inclusive scan with uniform x^(8*64*d) shifts combines the
+//    pieces of each packet.
+//
+// All algebra (tables, operators) is generated on the host in crc32_math.hpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "crc32_math.hpp"
+#include "wtp_crc32.h"
+
+namespace wtp {
+
+// ------------------------------------------------------------------------------------
+// Device constant tables (one block per device, built once on the host)
+// ------------------------------------------------------------------------------------
+constexpr int kG = 16;                       // lanes per packet in the braided kernel
+constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
+constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
+constexpr int kPieceS = 64;                  // piece bytes in the general kernel
+constexpr uint32_t kMaxVarLen = 4096;        // 64 pieces x 64 B: one packet per wave max
+
+constexpr uint32_t OFF_BRAID = 0;            // 4x256 braid word tables (advance 256 B)
+constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-256, x^-512, x^-1024
+constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
+constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
+constexpr uint32_t OFF_CINIT = OFF_FWD + 6 * 1024;  // init_const(L), L = 0..4096
+constexpr uint32_t TAB_WORDS = OFF_CINIT + kMaxVarLen + 4;
+
+// LDS images.  Replicated word tables: byte address
+//   t_hi*65536 + e*256 + t_lo*128 + (lane&31)*4   for table t = 2*t_hi + t_lo,
+// so a ds_read_b32 by lane L always lands in bank L%32 whatever the byte e.
+constexpr uint32_t kRepBytes = 131072;
+constexpr uint32_t kOpBytes = 4096;
+constexpr uint32_t kLdsWords = (kRepBytes + 6 * kOpBytes) / 4;  // 155,648 B
+
+namespace dev {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
+}
+
+// Copy four 256-entry word tables from global into the replicated LDS image.
+__device__ __forceinline__ void fill_replicated(char *lds, const uint32_t *__restrict__ g) {
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t t = i >> 8, e = i & 255u;
+        const uint32_t v = g[i];
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + (t >> 1) * 65536u + e * 256u + (t & 1u) * 128u);
+        const u32x4 q = {v, v, v, v};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dst[c] = q;
+    }
+}
+
+__device__ __forceinline__ void fill_ops(char *lds, const uint32_t *__restrict__ g, int nops) {
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kRepBytes);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(g);
+    for (int i = threadIdx.x; i < nops * 256; i += blockDim.x) dst[i] = src[i];
+}
+
+// Per-lane address constants for the replicated tables: byte0 = t_lo<<7 | (lane&31)<<2,
+// byte2 = t_hi.  v_perm_b32(x, K_t, sel_t) = K_t.b0 | x.b_t << 8 | K_t.b2 << 16.
+struct RepKeys {
+    uint32_t k[4];
+    __device__ __forceinline__ explicit RepKeys(uint32_t lane) {
+        const uint32_t c4 = (lane & 31u) << 2;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) k[t] = ((t & 1u) << 7) | c4 | ((t >> 1) << 16);
+    }
+};
+
+// XOR_t table_t[byte_t(x)] through the replicated image (4 v_perm + 4 ds_read_b32).
+__device__ __forceinline__ uint32_t rep_word(const char *lds, const RepKeys &K, uint32_t x) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, K.k[0], 0x0C020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, K.k[1], 0x0C020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, K.k[2], 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, K.k[3], 0x0C020700u);
+    return (lds_rd(lds, a0) ^ lds_rd(lds, a1)) ^ (lds_rd(lds, a2) ^ lds_rd(lds, a3));
+}
+
+// Table 3 of the slice-by-4 set is the plain Sarwate table: one byte step.
+__device__ __forceinline__ uint32_t rep_byte(const char *lds, const RepKeys &K, uint32_t c, uint32_t b) {
+    const uint32_t a = __builtin_amdgcn_perm((c ^ b), K.k[3], 0x0C020400u);
+    return lds_rd(lds, a) ^ (c >> 8);
+}
+
+// Linear operator stored as 4 byte tables at LDS byte offset `base`.
+__device__ __forceinline__ uint32_t op_apply(const char *lds, uint32_t base, uint32_t v) {
+    return (lds_rd(lds, base + ((v & 0xFFu) << 2)) ^ lds_rd(lds, base + 1024u + ((v >> 6) & 0x3FCu))) ^
+           (lds_rd(lds, base + 2048u + ((v >> 14) & 0x3FCu)) ^ lds_rd(lds, base + 3072u + ((v >> 22) & 0x3FCu)));
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// ------------------------------------------------------------------------------------
+// 1. braided fixed-length kernel
+// ------------------------------------------------------------------------------------
+// Packet p occupies base[p*stride, p*stride + len), (base + len) % 16 == 0,
+// stride % 16 == 0, len % 16 == 0, 256*(ROWS-1) < len <= 256*ROWS.
+// The packet is viewed right-aligned in a frame of ROWS x 256 bytes; the Z leading
+// 16-B chunks of the frame are virtual zeros (free: R_0(0^k || M) = R_0(M)).
+template <int ROWS>
+__global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint64_t stride,
+                                                      uint32_t len, uint64_t n, uint32_t *__restrict__ out,
+                                                      const uint32_t *__restrict__ gtab, uint32_t cinit) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    fill_replicated(lds, gtab + OFF_BRAID);
+    fill_ops(lds, gtab + OFF_INV, 6);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t nwave = blockDim.x >> 6;
+    const uint32_t j = lane & (kG - 1);  // braid group (column) within the packet
+    const uint32_t q = lane >> 4;        // packet slot within the wave (0..3)
+    const RepKeys K(lane);
+
+    constexpr uint32_t kFrame = 256u * ROWS;
+    const uint32_t zc = (kFrame - len) >> 4;  // leading virtual chunks
+    const uint64_t rounds = (n + 3) >> 2;
+
+    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+
+    // chunk (row i, column j) of packet p lives at  end(p) - kFrame + (i*16 + j)*16
+    auto load_round = [&](uint64_t rr, u32x4 (&w)[ROWS]) {
+        uint64_t p = rr * 4 + q;
+        p = p < n ? p : n - 1;  // clamp: tail lanes re-read a valid packet, result dropped
+        const uint8_t *fs = base + p * stride + len - kFrame;
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) {
+            const uint32_t c = uint32_t(i) * kG + j;
+            if (c >= zc)
+                w[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + c * 16u));
+            else
+                w[i] = u32x4{0, 0, 0, 0};
+        }
+    };
+
+    u32x4 nxt[ROWS];
+    if (r < rounds) load_round(r, nxt);
+    for (; r < rounds; r += rstep) {
+        u32x4 w[ROWS];
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) w[i] = nxt[i];
+        if (r + rstep < rounds) load_round(r + rstep, nxt);
+
+        uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) {
+            b0 = rep_word(lds, K, b0 ^ w[i].x);
+            b1 = rep_word(lds, K, b1 ^ w[i].y);
+            b2 = rep_word(lds, K, b2 ^ w[i].z);
+            b3 = rep_word(lds, K, b3 ^ w[i].w);
+        }
+        // braid b = 4j + k holds R_0(frame_b) * x^(32 b): fold with x^(-32 k), then
+        // across lanes with x^(-128 j).
+        uint32_t v = b0 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b1) ^
+                     op_apply(lds, kRepBytes + 1 * kOpBytes, b2 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b3));
+#pragma unroll
+        for (uint32_t d = 1, o = 2; d < kG; d <<= 1, ++o) {
+            const uint32_t u = __shfl_down(v, d, kG);
+            if ((j & (2 * d - 1)) == 0) v ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
+        }
+        const uint64_t p = r * 4 + q;
+        if (j == 0 && p < n) out[p] = v ^ cinit;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// 2. pieces kernel (general shapes)
+// ------------------------------------------------------------------------------------
+struct CrcEpi {
+    uint32_t *__restrict__ out;
+    __device__ __forceinline__ void put(const uint8_t *, uint64_t p, uint64_t, uint32_t crc, bool) const {
+        out[p] = crc;
+    }
+};
+struct VerifyEpi {  // Receiver.cpp:203-206: (int)ntohl(hdr.checksum) == (int)crc32(payload)
+    uint8_t *__restrict__ ok_out;
+    uint32_t *__restrict__ crc_out;  // may be null
+    __device__ __forceinline__ void put(const uint8_t *base, uint64_t p, uint64_t off, uint32_t crc,
+                                        bool valid) const {
+        bool ok = false;
+        if (valid) {
+            const uint8_t *h = base + off - 4;  // header.checksum, big-endian on the wire
+            const uint32_t want = (uint32_t(h[0]) << 24) | (uint32_t(h[1]) << 16) | (uint32_t(h[2]) << 8) | h[3];
+            ok = want == crc;
+        } else {
+            crc = 0;
+        }
+        ok_out[p] = ok ? 1 : 0;
+        if (crc_out) crc_out[p] = crc;
+    }
+};
+
+// Buffer resource over [base, base + nbytes) (nbytes rounded up to 16 by the host, so
+// every 16-B block that holds a valid byte is in range); out-of-range loads return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+template <class Prov, class Epi>
+__global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
+                                                 uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
+                                                 uint32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    fill_replicated(lds, gtab + OFF_S4);
+    fill_ops(lds, gtab + OFF_FWD, 6);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t gw = uint64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t tw = uint64_t(gridDim.x) * (blockDim.x >> 6);
+    const uint64_t lo = n * gw / tw, hi = n * (gw + 1) / tw;
+    const RepKeys K(lane);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
+
+    for (uint64_t p0 = lo; p0 < hi;) {
+        // --- this round's packets: lane i describes packet p0 + i ----------------------
+        const uint64_t pi = p0 + lane;
+        const bool have = pi < hi;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        bool valid = false;
+        if (have) prov.get(pi, off, len, valid);
+        if (have && len > kMaxVarLen) {
+            atomicOr(status, 1u);
+            len = 0;
+            valid = false;
+        }
+        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 65u;
+        uint32_t incl = k;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(incl, d);
+            if (lane >= d) incl += u;
+        }
+        const uint64_t fitmask = __ballot(have && incl <= 64u);
+        const uint32_t m = __popcll(fitmask);  // >= 1: a packet has <= 64 pieces
+        const uint32_t total = __shfl(incl, m - 1);
+
+        // --- lane -> (packet, piece): pk = #packets whose pieces all precede this lane -
+        uint32_t pk = 0;
+#pragma unroll
+        for (uint32_t s = 32; s >= 1; s >>= 1) {
+            const uint32_t probe = pk + s - 1;
+            const uint32_t v = __shfl(incl, probe & 63u);
+            if (probe < m && v <= lane) pk += s;
+        }
+        const bool active = lane < total;
+        pk = active ? pk : 0;
+        const uint32_t pinc = __shfl(incl, pk);
+        const uint32_t pkk = __shfl(k, pk);
+        const uint32_t plen = __shfl(len, pk);
+        const uint32_t poff_lo = __shfl(uint32_t(off), pk);
+        const uint32_t poff_hi = __shfl(uint32_t(off >> 32), pk);
+        const bool pvalid = __shfl(valid ? 1u : 0u, pk) != 0;
+        const uint64_t poff = (uint64_t(poff_hi) << 32) | poff_lo;
+        const uint32_t piece = lane - (pinc - pkk);  // 0 = head piece
+
+        // --- piece window: the 64 bytes ending at this piece's end ----------------------
+        // Pieces are counted back from the packet end, so every window is exactly 64 B;
+        // the head window also covers up to 64 bytes before the packet, which are
+        // masked to zero (free: R_0(0^k || M) = R_0(M)).
+        const int64_t we = int64_t(poff + plen) - int64_t(pkk - 1 - piece) * kPieceS;
+        const int64_t ws = we - kPieceS;
+        const int64_t vf64 = int64_t(poff) - ws;  // bytes of the window before the packet
+        const int32_t vf = active ? int32_t(vf64 > 64 ? 64 : vf64) : 64;
+        const uint32_t a = uint32_t(uint64_t(ws) & 15u);
+        const uint32_t blk = uint32_t(uint64_t(ws - int64_t(a)));  // may wrap: OOB -> 0
+
+        uint32_t d[20];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            u32x4 x = {0, 0, 0, 0};
+            if (active && vf < 16 * (u + 1)) x = buf_ld16(rs, blk + 16u * u);
+            d[4 * u + 0] = x.x;
+            d[4 * u + 1] = x.y;
+            d[4 * u + 2] = x.z;
+            d[4 * u + 3] = x.w;
+        }
+        // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
+        const uint32_t m2 = 0u - ((a >> 3) & 1u), m1 = 0u - ((a >> 2) & 1u), sb = a & 3u;
+        uint32_t e[18];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) e[i] = d[i] ^ ((d[i] ^ d[i + 2]) & m2);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
+
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
+            // keep bytes at window offset >= vf
+            const int32_t sh = vf - 4 * i;
+            const uint32_t keep = sh <= 0 ? 0xFFFFFFFFu : (sh >= 4 ? 0u : (0xFFFFFFFFu << (8 * sh)));
+            wd &= keep;
+            c = rep_word(lds, K, c ^ wd);
+        }
+
+        // --- segmented inclusive scan: W_i <- W_{i-d} * x^(8*64*d) ^ W_i ---------------
+        uint32_t W = c;
+#pragma unroll
+        for (uint32_t dd = 1, o = 0; dd < 64; dd <<= 1, ++o) {
+            const uint32_t u = __shfl_up(W, dd);
+            if (piece >= dd && lane >= dd) W ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
+        }
+        if (active && piece == pkk - 1) {
+            const uint32_t crc = W ^ gtab[OFF_CINIT + plen];
+            epi.put(base, p0 + pk, poff, crc, pvalid);
+        }
+        p0 += m;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// 3. fused DATA packet builder
+// ------------------------------------------------------------------------------------
+// Stage A: copy chunk i into its wire slot after a 16-B header hole; CRC computed on
+// the payload with the general kernel, then stage B writes the big-endian header.
+__global__ void k_wire_copy(const uint8_t *__restrict__ src, uint64_t total, uint8_t *__restrict__ wire,
+                            uint64_t wstride, uint64_t nchunks) {
+    const uint64_t per = WTP_MAX_PAYLOAD;
+    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;; t += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t i = t / (per / 4 + 1);  // 364 dwords + 1 header slot per chunk
+        if (i >= nchunks) break;
+        const uint64_t w = t % (per / 4 + 1);
+        if (w == per / 4) continue;
+        const uint64_t so = i * per + w * 4;
+        uint8_t *dst = wire + i * wstride + 16 + w * 4;
+        if (so + 4 <= total) {
+            uint32_t v;
+            memcpy(&v, src + so, 4);
+            memcpy(dst, &v, 4);
+        } else {
+            for (uint64_t b = so; b < total && b < so + 4; ++b) dst[b - so] = src[b];
+        }
+    }
+}
+__global__ void k_wire_header(const uint32_t *__restrict__ crc, uint64_t total, uint32_t seq0,
+                              uint8_t *__restrict__ wire, uint64_t wstride, uint32_t *__restrict__ wlen,
+                              uint64_t nchunks) {
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nchunks;
+         i += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t rem = total - i * WTP_MAX_PAYLOAD;
+        const uint32_t len = uint32_t(rem < WTP_MAX_PAYLOAD ? rem : WTP_MAX_PAYLOAD);
+        const uint32_t hdr[4] = {bswap32(WTP_TYPE_DATA), bswap32(seq0 + uint32_t(i)), bswap32(len), bswap32(crc[i])};
+        memcpy(wire + i * wstride, hdr, 16);
+        if (wlen) wlen[i] = 16 + len;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// 4. synthetic payload fill
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_synth(uint8_t *__restrict__ out, uint64_t start, uint64_t nbytes, uint64_t seed) {
+    const uint64_t w0 = start >> 3, w1 = (start + nbytes + 7) >> 3;
+    for (uint64_t w = w0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < w1;
+         w += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t z = mix64(seed + (w + 1) * 0x9E3779B97F4A7C15ull);
+        const uint64_t g0 = w << 3;
+        if (g0 >= start && g0 + 8 <= start + nbytes && ((reinterpret_cast<uintptr_t>(out + (g0 - start)) & 7u) == 0)) {
+            *reinterpret_cast<uint64_t *>(out + (g0 - start)) = z;
+        } else {
+            for (uint32_t b = 0; b < 8; ++b) {
+                const uint64_t g = g0 + b;
+                if (g >= start && g < start + nbytes) out[g - start] = uint8_t(z >> (8 * b));
+            }
+        }
+    }
+}
+
+}  // namespace dev
+
+// ------------------------------------------------------------------------------------
+// host side: per-device state, error handling, launchers
+// ------------------------------------------------------------------------------------
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define WTP_HIP(call)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) return fail(WTP_EHIP, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevState {
+    std::once_flag once;
+    int rc = WTP_OK;
+    std::string err;
+    uint32_t *tabs = nullptr;
+    uint32_t *status = nullptr;
+    int cus = 0;
+    std::mutex scratch_mu;
+    uint32_t *scratch = nullptr;
+    uint64_t scratch_words = 0;
+};
+constexpr int kMaxDev = 64;
+DevState g_dev[kMaxDev];
+
+std::vector<uint32_t> host_tables() {
+    std::vector<uint32_t> t(TAB_WORDS, 0);
+    make_word_tables(&t[OFF_BRAID], kBraidBlock);
+    const uint32_t inv_bytes[6] = {4, 8, 16, 32, 64, 128};
+    for (int o = 0; o < 6; ++o)
+        make_operator(&t[OFF_INV + 1024 * o], [&](uint32_t v) { return unshift_bytes(v, inv_bytes[o]); });
+    make_word_tables(&t[OFF_S4], 4);
+    for (int o = 0; o < 6; ++o) {
+        const uint64_t nb = uint64_t(kPieceS) << o;
+        make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
+    }
+    uint32_t ff = 0xFFFFFFFFu;  // init_const(L) incrementally
+    for (uint32_t L = 0; L <= kMaxVarLen; ++L) {
+        t[OFF_CINIT + L] = ff ^ 0xFFFFFFFFu;
+        ff = shift_bytes(ff, 1);
+    }
+    return t;
+}
+
+int init_device(int dev) {
+    if (dev < 0 || dev >= kMaxDev) return fail(WTP_EINVAL, "device %d out of range", dev);
+    DevState &s = g_dev[dev];
+    std::call_once(s.once, [&] {
+        auto setfail = [&](int code, const std::string &m) {
+            s.rc = code;
+            s.err = m;
+        };
+        int prev = 0;
+        hipGetDevice(&prev);
+        if (hipSetDevice(dev) != hipSuccess) return setfail(WTP_ENODEV, "hipSetDevice failed");
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return setfail(WTP_ENODEV, "hipGetDeviceProperties failed");
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return setfail(WTP_ENODEV, std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
+        s.cus = prop.multiProcessorCount;
+        std::vector<uint32_t> t = host_tables();
+        if (hipMalloc(&s.tabs, t.size() * 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(tables) failed");
+        if (hipMemcpy(s.tabs, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
+        if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
+        if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
+        hipSetDevice(prev);
+    });
+    if (s.rc != WTP_OK) return fail(s.rc, "wtp init(device %d): %s", dev, s.err.c_str());
+    return WTP_OK;
+}
+
+int current(DevState *&s) {
+    int dev = 0;
+    WTP_HIP(hipGetDevice(&dev));
+    int rc = init_device(dev);
+    if (rc) return rc;
+    s = &g_dev[dev];
+    return WTP_OK;
+}
+
+int launch_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WTP_EHIP, "launch %s: %s", what, hipGetErrorString(e));
+    return WTP_OK;
+}
+
+template <int ROWS>
+void launch_braid_rows(dim3 grid, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len, uint64_t n,
+                       uint32_t *out, const uint32_t *tabs, uint32_t cinit) {
+    hipLaunchKernelGGL(dev::k_fixed_braid<ROWS>, grid, dim3(1024), 0, st, b, stride, len, n, out, tabs, cinit);
+}
+
+int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
+                       uint32_t *out, hipStream_t st) {
+    const int rows = int((len + 255) / 256);
+    const uint64_t rounds = (n + 3) / 4;
+    const uint64_t want = (rounds + 15) / 16;
+    const unsigned grid = unsigned(want < uint64_t(s.cus) ? want : uint64_t(s.cus));
+    const uint32_t cinit = init_const(len);
+    switch (rows) {
+        case 1: launch_braid_rows<1>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 2: launch_braid_rows<2>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 3: launch_braid_rows<3>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 4: launch_braid_rows<4>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 5: launch_braid_rows<5>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 6: launch_braid_rows<6>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        default: return fail(WTP_EINVAL, "braid rows %d", rows);
+    }
+    return launch_check("k_fixed_braid");
+}
+
+template <class Prov, class Epi>
+int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, uint64_t n, Epi epi,
+                  hipStream_t st) {
+    // Align the buffer view down to 16 B and round its size up: every 16-B block holding
+    // a valid byte is then fully inside the resource (and inside one page).
+    const uintptr_t ub = reinterpret_cast<uintptr_t>(base);
+    const uint64_t lead = ub & 15u;
+    const uint8_t *b16 = base - lead;
+    const uint64_t span = (lead + nbytes + 15) & ~uint64_t(15);
+    if (span >= (1ull << 31)) return fail(WTP_EINVAL, "general kernel span %llu B >= 2 GiB (split the batch)", (unsigned long long)span);
+    const uint64_t waves_want = (n + 63) / 64;
+    uint64_t grid = (waves_want + 15) / 16;
+    if (grid > uint64_t(s.cus)) grid = uint64_t(s.cus);
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(1024), 0, st, b16, uint32_t(span),
+                       prov, n, epi, s.tabs, s.status);
+    return launch_check("k_pieces");
+}
+
+}  // namespace
+
+// Offsets handed to k_pieces must be relative to the 16-B aligned view.  The providers
+// below add `lead` back.
+namespace dev {
+struct FixedProvL {
+    uint64_t stride, lead;
+    uint32_t len;
+    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
+        off = lead + p * stride;
+        l = len;
+        ok = true;
+    }
+};
+struct ArrayProvL {
+    const uint64_t *__restrict__ offs;
+    const uint32_t *__restrict__ lens;
+    uint64_t lead;
+    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
+        off = lead + offs[p];
+        l = lens[p];
+        ok = true;
+    }
+};
+struct DgramProvL {
+    uint64_t stride, lead;
+    const uint32_t *__restrict__ rl;
+    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
+        const uint32_t r = rl[p];
+        off = lead + p * stride + 16;
+        ok = r >= 16 && r <= stride;
+        l = ok ? r - 16 : 0;
+    }
+};
+}  // namespace dev
+
+}  // namespace wtp
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+using namespace wtp;
+
+extern "C" {
+
+const char *wtp_version(void) { return "wtp-crc32-mi355x 0.1 (gfx950)"; }
+
+const char *wtp_last_error(void) { return g_err.c_str(); }
+
+int wtp_set_error_(int code, const char *msg) {
+    g_err = msg ? msg : "";
+    return code;
+}
+
+int wtp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int wtp_init(int device) { return init_device(device); }
+
+int wtp_device_status(int device, uint32_t *flags, int clear) {
+    if (!flags) return fail(WTP_EINVAL, "flags is null");
+    int rc = init_device(device);
+    if (rc) return rc;
+    int prev = 0;
+    WTP_HIP(hipGetDevice(&prev));
+    WTP_HIP(hipSetDevice(device));
+    WTP_HIP(hipDeviceSynchronize());
+    WTP_HIP(hipMemcpy(flags, g_dev[device].status, 4, hipMemcpyDeviceToHost));
+    if (clear) WTP_HIP(hipMemset(g_dev[device].status, 0, 4));
+    WTP_HIP(hipSetDevice(prev));
+    return WTP_OK;
+}
+
+uint32_t wtp_crc32(const void *buf, size_t size) {
+    return raw_update(0xFFFFFFFFu, static_cast<const uint8_t *>(buf), size) ^ 0xFFFFFFFFu;
+}
+
+int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, size_t n, uint32_t *d_out,
+                          void *stream) {
+    if (n == 0) return WTP_OK;
+    if (!d_out || (!d_payloads && len > 0)) return fail(WTP_EINVAL, "null pointer");
+    if (len > kMaxVarLen) return fail(WTP_EINVAL, "len %zu > %u", len, kMaxVarLen);
+    DevState *s = nullptr;
+    int rc = current(s);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t *b = static_cast<const uint8_t *>(d_payloads);
+    const bool fast = len >= 16 && len <= 1536 && len % 16 == 0 && stride % 16 == 0 &&
+                      (reinterpret_cast<uintptr_t>(b) + len) % 16 == 0;
+    if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, d_out, st);
+    // general kernel, in sub-batches whose byte span stays < 2 GiB
+    const uint64_t per = stride ? std::max<uint64_t>(1, ((1ull << 30) - 4096) / stride) : n;
+    for (uint64_t p = 0; p < n; p += per) {
+        const uint64_t cnt = std::min<uint64_t>(per, n - p);
+        const uint8_t *sb = b + p * stride;
+        const uint64_t lead = reinterpret_cast<uintptr_t>(sb) & 15u;
+        const uint64_t span = (cnt - 1) * stride + len;
+        rc = launch_pieces(*s, sb, span, dev::FixedProvL{stride, lead, uint32_t(len)}, cnt, dev::CrcEpi{d_out + p}, st);
+        if (rc) return rc;
+    }
+    return WTP_OK;
+}
+
+int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
+                        const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream) {
+    if (n == 0) return WTP_OK;
+    if (!d_base || !d_offsets || !d_lengths || !d_out) return fail(WTP_EINVAL, "null pointer");
+    DevState *s = nullptr;
+    int rc = current(s);
+    if (rc) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(d_base);
+    const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
+    return launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets, d_lengths, lead}, n, dev::CrcEpi{d_out},
+                         static_cast<hipStream_t>(stream));
+}
+
+int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len, size_t n,
+                           uint8_t *d_ok, uint32_t *d_crc_out, void *stream) {
+    if (n == 0) return WTP_OK;
+    if (!d_dgrams || !d_recv_len || !d_ok) return fail(WTP_EINVAL, "null pointer");
+    if (stride < 16) return fail(WTP_EINVAL, "stride %zu < 16", stride);
+    DevState *s = nullptr;
+    int rc = current(s);
+    if (rc) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(d_dgrams);
+    const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
+    const uint64_t span = uint64_t(n) * stride;
+    return launch_pieces(*s, b, span, dev::DgramProvL{stride, lead, d_recv_len}, n, dev::VerifyEpi{d_ok, d_crc_out},
+                         static_cast<hipStream_t>(stream));
+}
+
+int wtp_synth_fill(void *d_out, uint64_t start_byte, size_t nbytes, uint64_t seed, void *stream) {
+    if (nbytes == 0) return WTP_OK;
+    if (!d_out) return fail(WTP_EINVAL, "null pointer");
+    const uint64_t words = (nbytes + 16) / 8;
+    uint64_t blocks = (words + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(dev::k_synth, dim3(unsigned(blocks)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<uint8_t *>(d_out), start_byte, uint64_t(nbytes), seed);
+    return launch_check("k_synth");
+}
+
+int wtp_build_data_packets(const void *d_payloads, size_t total_bytes, uint32_t seq0, void *d_wire,
+                           size_t wire_stride, uint32_t *d_wire_len, void *stream) {
+    if (total_bytes == 0) return WTP_OK;
+    if (!d_payloads || !d_wire) return fail(WTP_EINVAL, "null pointer");
+    if (wire_stride < 16 + WTP_MAX_PAYLOAD) return fail(WTP_EINVAL, "wire_stride %zu < 1472", wire_stride);
+    DevState *s = nullptr;
+    int rc = current(s);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t nch = (total_bytes + WTP_MAX_PAYLOAD - 1) / WTP_MAX_PAYLOAD;
+    uint32_t *crc = d_wire_len;  // CRCs land here first, then become the lengths
+    if (!crc) {
+        std::lock_guard<std::mutex> g(s->scratch_mu);
+        if (s->scratch_words < nch) {
+            if (s->scratch) hipFree(s->scratch);
+            s->scratch = nullptr;
+            s->scratch_words = 0;
+            WTP_HIP(hipMalloc(&s->scratch, nch * 4));
+            s->scratch_words = nch;
+        }
+        crc = s->scratch;
+    }
+    uint8_t *wire = static_cast<uint8_t *>(d_wire);
+    {
+        const uint64_t work = nch * (WTP_MAX_PAYLOAD / 4 + 1);
+        uint64_t blocks = (work + 255) / 256;
+        if (blocks > 65536) blocks = 65536;
+        hipLaunchKernelGGL(dev::k_wire_copy, dim3(unsigned(blocks)), dim3(256), 0, st,
+                           static_cast<const uint8_t *>(d_payloads), uint64_t(total_bytes), wire, uint64_t(wire_stride), nch);
+        if ((rc = launch_check("k_wire_copy"))) return rc;
+    }
+    // CRC over the payloads in their wire slots (full chunks take the braided path when
+    // the slot layout is 16-B aligned, e.g. wire_stride 1472).
+    const uint64_t full = total_bytes / WTP_MAX_PAYLOAD;
+    const uint64_t tail = total_bytes - full * WTP_MAX_PAYLOAD;
+    if (full && (rc = wtp_crc32_batch_fixed(wire + 16, wire_stride, WTP_MAX_PAYLOAD, full, crc, stream))) return rc;
+    if (tail && (rc = wtp_crc32_batch_fixed(wire + full * wire_stride + 16, 0, tail, 1, crc + full, stream))) return rc;
+    {
+        uint64_t blocks = (nch + 255) / 256;
+        if (blocks > 65536) blocks = 65536;
+        hipLaunchKernelGGL(dev::k_wire_header, dim3(unsigned(blocks)), dim3(256), 0, st, crc, uint64_t(total_bytes),
+                           seq0, wire, uint64_t(wire_stride), d_wire_len, nch);
+        if ((rc = launch_check("k_wire_header"))) return rc;
+    }
+    return WTP_OK;
+}
+
+}  // extern "C"

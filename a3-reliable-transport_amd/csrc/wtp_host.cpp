@@ -1,0 +1,226 @@
+// wtp_host.cpp — host-memory entry points of the C-ABI (include/wtp_crc32.h).
+//
+// The reference path starts and ends in host memory: wSender reads the whole file into
+// a std::vector<char> and checksums it chunk by chunk (cpp/src/base/Sender.cpp:82-92),
+// wReceiver checksums each recvfrom() buffer (cpp/src/base/Receiver.cpp:123-131,
+// :203-206).  These wrappers move such host batches through the device kernels:
+//
+//   slab s (<= 64 MiB of payload) on stream s%2:
+//     [pageable source: CPU memcpy into library-owned pinned slab]  ->  H2D
+//     -> CRC kernel -> D2H of the 32-bit results into pinned memory
+//
+// Two slabs are in flight, so slab s+1's staging and H2D overlap slab s's kernel and
+// D2H.  Pinned sources (e.g. from hipHostMalloc) are copied H2D directly.  The end-to-end
+// rate is PCIe-bound; DESIGN.md records the measured figure.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "wtp_crc32.h"
+
+// Defined in crc32_kernels.hip: sets the per-thread message read by wtp_last_error().
+extern "C" int wtp_set_error_(int code, const char *msg);
+
+namespace {
+
+constexpr size_t kSlabBytes = 64ull << 20;
+
+int hfail(int code, const char *what, hipError_t e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    return wtp_set_error_(code, buf);
+}
+
+#define H_HIP(call)                                                  \
+    do {                                                             \
+        hipError_t e_ = (call);                                      \
+        if (e_ != hipSuccess) return hfail(WTP_EHIP, #call, e_);     \
+    } while (0)
+
+struct Pipe {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t st[2] = {nullptr, nullptr};
+    uint8_t *pin_in[2] = {nullptr, nullptr};
+    uint8_t *dev_in[2] = {nullptr, nullptr};
+    uint32_t *pin_aux[2] = {nullptr, nullptr};   // recv_len staging (verify)
+    uint32_t *dev_aux[2] = {nullptr, nullptr};
+    uint32_t *pin_out[2] = {nullptr, nullptr};   // crc results
+    uint32_t *dev_out[2] = {nullptr, nullptr};
+    uint8_t *pin_ok[2] = {nullptr, nullptr};
+    uint8_t *dev_ok[2] = {nullptr, nullptr};
+    size_t max_pk = 0;                           // packets per slab (results capacity)
+};
+Pipe g_pipe[64];
+
+int pipe_get(Pipe *&out) {
+    int dev = 0;
+    H_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return hfail(WTP_EINVAL, "device index", hipSuccess);
+    int rc = wtp_init(dev);
+    if (rc) return rc;
+    Pipe &p = g_pipe[dev];
+    if (!p.ready) {
+        p.max_pk = kSlabBytes / 16 + 1;  // worst case: 16-B datagrams / 1-B chunks capped below
+        for (int b = 0; b < 2; ++b) {
+            H_HIP(hipStreamCreateWithFlags(&p.st[b], hipStreamNonBlocking));
+            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_in[b]), kSlabBytes, hipHostMallocDefault));
+            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_in[b]), kSlabBytes + 64));
+            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_out[b]), p.max_pk * 4, hipHostMallocDefault));
+            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_out[b]), p.max_pk * 4));
+            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_aux[b]), p.max_pk * 4, hipHostMallocDefault));
+            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_aux[b]), p.max_pk * 4));
+            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_ok[b]), p.max_pk, hipHostMallocDefault));
+            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_ok[b]), p.max_pk));
+        }
+        p.ready = true;
+    }
+    out = &p;
+    return WTP_OK;
+}
+
+bool is_pinned(const void *ptr) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// One slab of work: `in_bytes` host bytes at `src` -> device, then `run` launches the
+// kernels on stream st; `finish` copies results out once the slab's stream is done.
+struct Slab {
+    const uint8_t *src = nullptr;
+    size_t in_bytes = 0;
+    size_t first = 0, count = 0;  // packet range
+    bool live = false;
+};
+
+}  // namespace
+
+extern "C" {
+
+// Fixed-geometry host batch (also used by wtp_crc32_host_chunked): payload i =
+// h[i*stride, i*stride + len), the last packet may be shorter (tail_len) when
+// `tail_len` != len.
+static int host_fixed_impl(const void *h_payloads, size_t stride, size_t len, size_t n, size_t tail_len,
+                           uint32_t *h_out) {
+    if (n == 0) return WTP_OK;
+    if (!h_payloads || !h_out) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (len > kSlabBytes || stride > kSlabBytes) return hfail(WTP_EINVAL, "payload/stride larger than a slab", hipSuccess);
+    Pipe *P = nullptr;
+    int rc = pipe_get(P);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(P->mu);
+    const uint8_t *h = static_cast<const uint8_t *>(h_payloads);
+    const bool pinned = is_pinned(h_payloads);
+    const size_t step = stride ? stride : 1;
+    size_t per = std::min(P->max_pk, std::max<size_t>(1, (kSlabBytes - len) / step + 1));
+    if (stride == 0) per = std::min(n, P->max_pk);
+    Slab slot[2];
+    size_t s = 0;
+    for (size_t first = 0; first < n || slot[0].live || slot[1].live; ++s) {
+        const int b = int(s & 1);
+        Slab &sl = slot[b];
+        if (sl.live) {  // retire the slab that used this buffer two steps ago
+            H_HIP(hipStreamSynchronize(P->st[b]));
+            memcpy(h_out + sl.first, P->pin_out[b], sl.count * 4);
+            sl.live = false;
+        }
+        if (first >= n) continue;
+        const size_t cnt = std::min(per, n - first);
+        const bool has_tail = (first + cnt == n) && tail_len != len;
+        const size_t last_len = has_tail ? tail_len : len;
+        const size_t bytes = (cnt - 1) * stride + last_len;
+        const uint8_t *src = h + first * stride;
+        if (pinned) {
+            H_HIP(hipMemcpyAsync(P->dev_in[b], src, bytes, hipMemcpyHostToDevice, P->st[b]));
+        } else {
+            memcpy(P->pin_in[b], src, bytes);
+            H_HIP(hipMemcpyAsync(P->dev_in[b], P->pin_in[b], bytes, hipMemcpyHostToDevice, P->st[b]));
+        }
+        const size_t full = has_tail ? cnt - 1 : cnt;
+        if (full && (rc = wtp_crc32_batch_fixed(P->dev_in[b], stride, len, full, P->dev_out[b], P->st[b]))) return rc;
+        if (has_tail &&
+            (rc = wtp_crc32_batch_fixed(P->dev_in[b] + full * stride, 0, tail_len, 1, P->dev_out[b] + full, P->st[b])))
+            return rc;
+        H_HIP(hipMemcpyAsync(P->pin_out[b], P->dev_out[b], cnt * 4, hipMemcpyDeviceToHost, P->st[b]));
+        sl.first = first;
+        sl.count = cnt;
+        sl.live = true;
+        first += cnt;
+    }
+    return WTP_OK;
+}
+
+int wtp_crc32_host_batch_fixed(const void *h_payloads, size_t stride, size_t len, size_t n, uint32_t *h_out) {
+    return host_fixed_impl(h_payloads, stride, len, n, len, h_out);
+}
+
+int wtp_crc32_host_chunked(const void *h_buf, size_t nbytes, size_t chunk, uint32_t *h_out) {
+    if (nbytes == 0) return WTP_OK;
+    if (chunk == 0) return hfail(WTP_EINVAL, "chunk == 0", hipSuccess);
+    const size_t n = (nbytes + chunk - 1) / chunk;
+    const size_t tail = nbytes - (n - 1) * chunk;
+    return host_fixed_impl(h_buf, chunk, chunk, n, tail, h_out);
+}
+
+int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len, size_t n, uint8_t *h_ok,
+                          uint32_t *h_crc_out) {
+    if (n == 0) return WTP_OK;
+    if (!h_dgrams || !h_recv_len || !h_ok) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (stride < 16 || stride > kSlabBytes) return hfail(WTP_EINVAL, "bad datagram stride", hipSuccess);
+    Pipe *P = nullptr;
+    int rc = pipe_get(P);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(P->mu);
+    const uint8_t *h = static_cast<const uint8_t *>(h_dgrams);
+    const size_t per = std::min(P->max_pk, kSlabBytes / stride);
+    Slab slot[2];
+    size_t s = 0;
+    for (size_t first = 0; first < n || slot[0].live || slot[1].live; ++s) {
+        const int b = int(s & 1);
+        Slab &sl = slot[b];
+        if (sl.live) {
+            H_HIP(hipStreamSynchronize(P->st[b]));
+            memcpy(h_ok + sl.first, P->pin_ok[b], sl.count);
+            if (h_crc_out) memcpy(h_crc_out + sl.first, P->pin_out[b], sl.count * 4);
+            sl.live = false;
+        }
+        if (first >= n) continue;
+        const size_t cnt = std::min(per, n - first);
+        memcpy(P->pin_in[b], h + first * stride, cnt * stride);
+        memcpy(P->pin_aux[b], h_recv_len + first, cnt * 4);
+        H_HIP(hipMemcpyAsync(P->dev_in[b], P->pin_in[b], cnt * stride, hipMemcpyHostToDevice, P->st[b]));
+        H_HIP(hipMemcpyAsync(P->dev_aux[b], P->pin_aux[b], cnt * 4, hipMemcpyHostToDevice, P->st[b]));
+        if ((rc = wtp_crc32_verify_batch(P->dev_in[b], stride, P->dev_aux[b], cnt, P->dev_ok[b], P->dev_out[b], P->st[b])))
+            return rc;
+        H_HIP(hipMemcpyAsync(P->pin_ok[b], P->dev_ok[b], cnt, hipMemcpyDeviceToHost, P->st[b]));
+        H_HIP(hipMemcpyAsync(P->pin_out[b], P->dev_out[b], cnt * 4, hipMemcpyDeviceToHost, P->st[b]));
+        sl.first = first;
+        sl.count = cnt;
+        sl.live = true;
+        first += cnt;
+    }
+    return WTP_OK;
+}
+
+// Pinned host allocation helpers for callers that want zero-copy staging (wSender reads
+// its file straight into such a buffer).
+void *wtp_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+void wtp_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+}  // extern "C"

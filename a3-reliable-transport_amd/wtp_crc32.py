@@ -1,0 +1,179 @@
+"""ctypes binding of the product C-ABI (include/wtp_crc32.h -> lib/libwtp_crc32.so).
+
+This is plumbing for tests and bench.py: every call goes straight to the HIP library.
+There is no CPU fallback — if the library is missing or fails to load, import raises.
+
+Device buffers are torch tensors (torch is used only for device memory and streams);
+`stream` defaults to torch's current stream, so torch.cuda.Event timing sees the
+launches.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libwtp_crc32.so")
+
+MAX_PAYLOAD = 1456
+MAX_KERNEL_LEN = 4096
+
+
+class WtpError(RuntimeError):
+    pass
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise WtpError(f"HIP library not built: {LIB_PATH} (run `make -C a3-reliable-transport_amd lib` "
+                       "or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
+    sig = {
+        "wtp_version": (C.c_char_p, []),
+        "wtp_last_error": (C.c_char_p, []),
+        "wtp_device_count": (i32, []),
+        "wtp_init": (i32, [i32]),
+        "wtp_device_status": (i32, [i32, C.POINTER(u32), i32]),
+        "wtp_crc32": (u32, [vp, sz]),
+        "wtp_crc32_batch_fixed": (i32, [vp, sz, sz, sz, vp, vp]),
+        "wtp_crc32_batch_var": (i32, [vp, sz, vp, vp, sz, vp, vp]),
+        "wtp_crc32_verify_batch": (i32, [vp, sz, vp, sz, vp, vp, vp]),
+        "wtp_build_data_packets": (i32, [vp, sz, u32, vp, sz, vp, vp]),
+        "wtp_crc32_host_batch_fixed": (i32, [vp, sz, sz, sz, vp]),
+        "wtp_crc32_host_chunked": (i32, [vp, sz, sz, vp]),
+        "wtp_crc32_host_verify": (i32, [vp, sz, vp, sz, vp, vp]),
+        "wtp_host_alloc": (vp, [sz]),
+        "wtp_host_free": (None, [vp]),
+        "wtp_synth_fill": (i32, [vp, u64, sz, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+LIB = _load()
+EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_crc32",
+            "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_verify_batch", "wtp_build_data_packets",
+            "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_verify", "wtp_host_alloc",
+            "wtp_host_free", "wtp_synth_fill")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise WtpError(f"{what} failed ({rc}): {LIB.wtp_last_error().decode()}")
+
+
+def _dptr(t) -> int:
+    """Device pointer of a torch tensor (or an int)."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    if not t.is_cuda:
+        raise WtpError("expected a device tensor")
+    if not t.is_contiguous():
+        raise WtpError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _stream(stream):
+    if stream is not None:
+        return stream if isinstance(stream, int) else stream.cuda_stream
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ---- CPU single-packet semantics (Crc32.hpp:91-102) --------------------------------
+def crc32(data) -> int:
+    b = bytes(data)
+    buf = C.create_string_buffer(b, len(b)) if b else None
+    return int(LIB.wtp_crc32(buf, len(b)))
+
+
+# ---- device batches ----------------------------------------------------------------
+def crc32_batch_fixed(payloads, stride: int, length: int, n: int, out, stream=None) -> None:
+    _check(LIB.wtp_crc32_batch_fixed(_dptr(payloads), stride, length, n, _dptr(out), _stream(stream)),
+           "wtp_crc32_batch_fixed")
+
+
+def crc32_batch_var(base, base_bytes: int, offsets, lengths, n: int, out, stream=None) -> None:
+    _check(LIB.wtp_crc32_batch_var(_dptr(base), base_bytes, _dptr(offsets), _dptr(lengths), n, _dptr(out),
+                                   _stream(stream)), "wtp_crc32_batch_var")
+
+
+def verify_batch(dgrams, stride: int, recv_len, n: int, ok, crc_out=None, stream=None) -> None:
+    _check(LIB.wtp_crc32_verify_batch(_dptr(dgrams), stride, _dptr(recv_len), n, _dptr(ok), _dptr(crc_out),
+                                      _stream(stream)), "wtp_crc32_verify_batch")
+
+
+def build_data_packets(payloads, total_bytes: int, seq0: int, wire, wire_stride: int, wire_len=None,
+                       stream=None) -> None:
+    _check(LIB.wtp_build_data_packets(_dptr(payloads), total_bytes, seq0, _dptr(wire), wire_stride,
+                                      _dptr(wire_len), _stream(stream)), "wtp_build_data_packets")
+
+
+def synth_fill(out, start_byte: int = 0, seed: int = 0x5EED, nbytes: int | None = None, stream=None) -> None:
+    nb = out.numel() * out.element_size() if nbytes is None else nbytes
+    _check(LIB.wtp_synth_fill(_dptr(out), start_byte, nb, seed, _stream(stream)), "wtp_synth_fill")
+
+
+def device_status(device: int = 0, clear: bool = True) -> int:
+    f = C.c_uint32(0)
+    _check(LIB.wtp_device_status(device, C.byref(f), 1 if clear else 0), "wtp_device_status")
+    return int(f.value)
+
+
+# ---- host-memory wrappers ------------------------------------------------------------
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def host_batch_fixed(buf: np.ndarray, stride: int, length: int, n: int) -> np.ndarray:
+    out = np.zeros(n, dtype=np.uint32)
+    _check(LIB.wtp_crc32_host_batch_fixed(_np_ptr(buf), stride, length, n, _np_ptr(out)), "host_batch_fixed")
+    return out
+
+
+def host_chunked(buf: np.ndarray, chunk: int = MAX_PAYLOAD, nbytes: int | None = None) -> np.ndarray:
+    nb = buf.nbytes if nbytes is None else nbytes
+    out = np.zeros((nb + chunk - 1) // chunk, dtype=np.uint32)
+    _check(LIB.wtp_crc32_host_chunked(_np_ptr(buf), nb, chunk, _np_ptr(out)), "host_chunked")
+    return out
+
+
+def host_verify(dgrams: np.ndarray, stride: int, recv_len: np.ndarray):
+    recv_len = np.ascontiguousarray(recv_len, dtype=np.uint32)
+    n = recv_len.size
+    ok = np.zeros(n, dtype=np.uint8)
+    crc = np.zeros(n, dtype=np.uint32)
+    _check(LIB.wtp_crc32_host_verify(_np_ptr(dgrams), stride, _np_ptr(recv_len), n, _np_ptr(ok), _np_ptr(crc)),
+           "host_verify")
+    return ok, crc
+
+
+class PinnedBuffer:
+    """Page-locked host buffer from the library (wtp_host_alloc) viewed as numpy uint8."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = LIB.wtp_host_alloc(nbytes)
+        if not self.ptr:
+            raise WtpError("wtp_host_alloc failed")
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            LIB.wtp_host_free(self.ptr)
+            self.ptr = None
+            self.array = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

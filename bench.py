@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py — WTP CRC-32 hot path on MI355X (BASELINE.json metric).
+
+One "step" = one pass of the hot path over one batch of synthetic, device-resident
+1456-byte DATA payloads: the braided CRC kernel over this rank's shard, plus (N > 1)
+the RCCL gather of the 32-bit results to rank 0.  Weak scaling: every rank owns
+--packets-per-rank packets (default 1 M = the north-star 1 M x 1456 target at N = 1;
+--packets-per-rank 2097152 at N = 8 is config C4, 16 M packets).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  value = GiB/s of payload over all ranks (whole job, max
+time over ranks); roofline = the CRC kernel's algorithmic read bytes per launch / its
+mean HIP-event duration vs the 8 TB/s HBM peak; cpu_baseline = the reference's own
+crc32 (oracle/_ref, compiled from cpp/src/common/Crc32.hpp) timed on this host's
+cores over a bounded sample of the same payloads.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "a3-reliable-transport_amd")
+sys.path.insert(0, PKG)
+
+PAYLOAD = 1456
+SEED = 0x5EED
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "GiB/s CRC-32 over device-resident 1456-B payloads; % of HBM read roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0,
+                    help="target wall seconds of each CPU-baseline leg (1 thread, all threads)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL gather inside the step")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_sample: int, seconds: float, threads: int) -> dict:
+    """Reference crc32 (oracle/_ref) or, if it was not built, the oracle port."""
+    import ctypes as C
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    ref = O.ref_lib()
+    kind = "reference" if ref is not None else "port"
+    buf = O.synth_fill_np(n_sample * PAYLOAD)
+    out = np.zeros(n_sample, dtype=np.uint32)
+    outp = out.ctypes.data_as(C.POINTER(C.c_uint32))
+
+    def run(nthreads: int) -> float:
+        if ref is not None:
+            if nthreads == 1:
+                ref.ref_crc32_batch_fixed(buf.ctypes.data, PAYLOAD, PAYLOAD, n_sample, outp)
+            else:
+                ref.ref_crc32_batch_fixed_mt(buf.ctypes.data, PAYLOAD, PAYLOAD, n_sample, outp, nthreads)
+        else:
+            O.lib().oracle_crc32_batch_fixed_mt(buf.ctypes.data, PAYLOAD, PAYLOAD, n_sample, outp, nthreads)
+        return float(n_sample * PAYLOAD)
+
+    res = {}
+    for nt in (1, threads):
+        run(nt)  # warm
+        done, t0 = 0.0, time.perf_counter()
+        while True:
+            done += run(nt)
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        res[nt] = (done / el / 2**30, done, el)
+    # sanity: the baseline computes the same CRCs as the oracle
+    assert out[0] == O.crc32(buf[:PAYLOAD]) and out[-1] == O.crc32(buf[-PAYLOAD:])
+    v1, vn = res[1], res[threads]
+    return {
+        "value": round(vn[0], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": f"{n_sample} x {PAYLOAD} B synthetic packets (seed 0x5EED), looped for ~{seconds:.0f} s per leg; "
+                  f"{kind} = {'cpp/src/common/Crc32.hpp:91-102 compiled -O2 (oracle/_ref)' if ref else 'oracle/crc32_oracle.c'}",
+        "value_1core": round(v1[0], 4),
+        "cpu_seconds": round(v1[2] + vn[2] * threads, 1),
+    }
+
+
+def pmc_traffic(n_packets: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("packets", -1)) == n_packets:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import shard
+    import wtp_crc32 as W
+
+    n = args.packets_per_rank
+    nbytes = n * PAYLOAD
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if W.LIB.wtp_init(torch.cuda.current_device()) != 0:
+        raise W.WtpError(W.LIB.wtp_last_error().decode())
+    stream = torch.cuda.current_stream()
+
+    # this rank's contiguous shard of the global packet stream, generated on-device
+    buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+    W.synth_fill(buf, start_byte=rank * nbytes, seed=SEED, nbytes=nbytes)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    do_gather = world > 1 and not args.no_gather
+
+    def step():
+        W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
+        if do_gather:
+            shard.gather_crcs(out, world, rank)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
+        ends[i].record(stream)
+        if do_gather:
+            shard.gather_crcs(out, world, rank)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    kmean = sum(kern_ms) / len(kern_ms)
+
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # spot parity vs the oracle (rank 0 checks its own first and last packets)
+    spot = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+        import oracle as O
+        got = out.cpu().numpy().view(np.uint32)
+        spot = all(int(got[i]) == O.crc32(O.synth_fill_np(PAYLOAD, start_byte=i * PAYLOAD)) for i in (0, 1, n // 2, n - 1))
+
+    total_bytes = float(nbytes) * world * args.steps
+    value = total_bytes / el / 2**30
+    achieved = nbytes / (kmean * 1e-3) / 1e9  # GB/s, algorithmic read bytes per launch
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 seed 0x5EED, generated on-device per rank shard)",
+        "config": {"workload": f"crc32 of {n} x {PAYLOAD}-B DATA payloads per GPU, device-resident"
+                               + (" + RCCL gather of u32 results to rank 0" if do_gather else ""),
+                   "packets_per_rank": n, "payload_bytes": PAYLOAD, "global_packets": n * world,
+                   "parallelism": f"packet shards x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(n),
+                     "kernel": "k_fixed_braid<6>", "kernel_ms_mean": round(kmean, 5),
+                     "kernel_ms_p10": round(kern_ms[len(kern_ms) // 10], 5),
+                     "kernel_ms_p90": round(kern_ms[(9 * len(kern_ms)) // 10], 5),
+                     "bytes_per_launch": nbytes},
+        "pct_hbm_read_roofline": round(100 * achieved / HBM_PEAK_GBS, 2),
+        "parity_spot_check": spot,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(65536, args.cpu_seconds, threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,73 @@
+"""C-ABI checks that need no GPU: the library loads, exports every entry point that
+include/wtp_crc32.h declares, validates arguments before touching a device, and its
+CPU crc32 (Crc32.hpp:91-102 semantics) matches the golden vectors."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "wtp_crc32.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(wtp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("wtp_crc32", "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_verify_batch",
+                 "wtp_crc32_host_chunked", "wtp_last_error", "wtp_build_data_packets"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    import wtp_crc32 as W
+    for name in declared_functions():
+        assert hasattr(W.LIB, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", W.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (wtp_\w+)", out))
+    missing = set(declared_functions()) - exported
+    assert not missing, missing
+    assert set(W.EXPORTED) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    import wtp_crc32 as W
+    blob = open(W.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_cpu_crc32_golden(golden):
+    import wtp_crc32 as W
+    assert W.crc32(b"123456789") == 0xCBF43926
+    assert W.crc32(b"") == 0
+    for L in (0, 1, 100, 1456):
+        import oracle as O
+        m = O.synth_fill_np(L, start_byte=1000 * L).tobytes()
+        assert W.crc32(m) == golden["per_length"]["crc"][L]
+
+
+def test_argument_validation_without_device():
+    import wtp_crc32 as W
+    L = W.LIB
+    out = C.c_uint32(0)
+    # n == 0: nothing to do, no device touched
+    assert L.wtp_crc32_batch_fixed(None, 1456, 1456, 0, None, None) == 0
+    assert L.wtp_crc32_batch_var(None, 0, None, None, 0, None, None) == 0
+    assert L.wtp_crc32_verify_batch(None, 1472, None, 0, None, None, None) == 0
+    # null pointers with n > 0 -> WTP_EINVAL (-1) and a message
+    assert L.wtp_crc32_batch_fixed(None, 1456, 1456, 4, C.addressof(out), None) == -1
+    assert b"null" in L.wtp_last_error()
+    assert L.wtp_crc32_batch_fixed(C.addressof(out), 1456, 5000, 4, C.addressof(out), None) == -1
+    assert L.wtp_crc32_verify_batch(C.addressof(out), 8, C.addressof(out), 1, C.addressof(out), None, None) == -1
+    assert L.wtp_crc32_host_chunked(C.addressof(out), 10, 0, C.addressof(out)) == -1
+
+
+def test_version_string():
+    import wtp_crc32 as W
+    assert b"gfx950" in W.LIB.wtp_version()

@@ -1,0 +1,313 @@
+"""GPU parity: every HIP entry point vs the CPU oracle, bit-exact, through the C-ABI.
+
+Sizes the oracle finishes in seconds are compared element-wise; the full 1M x 1456
+target size is checked through properties (two independent kernels agree on every
+packet, sampled packets vs the oracle, CRC-of-CRCs).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def W():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import wtp_crc32 as W
+    assert W.LIB.wtp_init(0) == 0, W.LIB.wtp_last_error()
+    return W
+
+
+def dev_u8(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8)).cuda()
+
+
+def u32_out(n):
+    return torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
+
+
+def to_u32(t, n):
+    torch.cuda.synchronize()
+    return t[:n].cpu().numpy().view(np.uint32)
+
+
+# ---- fixed length, braided fast path ---------------------------------------------------
+def test_c2_64k_x_1456_bit_exact(W):
+    n = 65536
+    buf = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = u32_out(n)
+    W.crc32_batch_fixed(buf, 1456, 1456, n, out)
+    got = to_u32(out, n)
+    host = O.synth_fill_np(n * 1456)
+    assert np.array_equal(buf.cpu().numpy(), host), "device synth fill != oracle generator"
+    want = O.batch_fixed(host, 1456, 1456, n, threads=8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}"
+
+
+def test_golden_batch_digest(W, golden):
+    g = golden["batch_4096x1456"]
+    buf = torch.empty(4096 * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = u32_out(4096)
+    W.crc32_batch_fixed(buf, 1456, 1456, 4096, out)
+    got = to_u32(out, 4096)
+    assert [f"0x{c:08X}" for c in got[:8]] == g["first8"]
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_le_u32"]
+
+
+@pytest.mark.parametrize("L", [16, 240, 256, 272, 512, 1024, 1280, 1296, 1440, 1456, 1536])
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 257, 4099])
+def test_fast_path_lengths_and_tails(W, L, n):
+    stride = ((L + 15) // 16) * 16 + 32 * (n % 2)  # stride > len on odd n
+    host = O.synth_fill_np(n * stride, start_byte=L * 7 + n)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_fixed(d, stride, L, n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_fixed(host, stride, L, n))
+
+
+def test_input_files_through_device(W, golden, golden_dir):
+    for name, f in golden["files"].items():
+        data = np.frombuffer(open(os.path.join(golden_dir, name), "rb").read(), dtype=np.uint8)
+        n = len(f["chunk_lens"])
+        full = data.size // 1456
+        d = dev_u8(np.concatenate([data, np.zeros(16, np.uint8)]))
+        out = u32_out(n)
+        if full:
+            W.crc32_batch_fixed(d, 1456, 1456, full, out)
+        if n > full:
+            W.crc32_batch_fixed(d[full * 1456:], 0, data.size - full * 1456, 1, out[full:])
+        assert [f"0x{c:08X}" for c in to_u32(out, n)] == f["crc"], name
+
+
+# ---- general kernel: every length, odd strides/alignments ------------------------------
+def test_every_length_0_to_1456_var(W, golden):
+    pl = golden["per_length"]["crc"]
+    lens = np.arange(1457, dtype=np.uint32)
+    offs = (1000 * lens).astype(np.uint64)
+    total = int(offs[-1] + lens[-1]) + 16
+    host = O.synth_fill_np(total)
+    d = dev_u8(host)
+    out = u32_out(1457)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), 1457, out)
+    got = to_u32(out, 1457)
+    assert list(got) == pl
+
+
+def test_every_length_fixed_entry(W, golden):
+    pl = golden["per_length"]["crc"]
+    host = O.synth_fill_np(1457 * 1000 + 1460)
+    d = dev_u8(host)
+    out = u32_out(1)
+    for L in range(0, 1457):
+        W.crc32_batch_fixed(d[1000 * L:], 0, L, 1, out)
+        got = to_u32(out, 1)[0]
+        assert got == pl[L], L
+
+
+@pytest.mark.parametrize("L,stride,lead", [(1455, 1455, 0), (1456, 1457, 3), (1456, 1456, 5), (100, 101, 1),
+                                           (1, 1, 0), (0, 7, 0), (64, 64, 9), (65, 80, 15), (4096, 4100, 2),
+                                           (1456, 1472, 8), (1484, 1500, 0)])
+def test_general_strides_and_alignment(W, L, stride, lead):
+    n = 777
+    host = O.synth_fill_np(lead + n * stride + L + 16, start_byte=L + stride)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_fixed(d[lead:], stride, L, n, out)
+    want = O.batch_fixed(host[lead:], stride, L, n)
+    assert np.array_equal(to_u32(out, n), want)
+
+
+def test_zipf_mixed_lengths(W):
+    n = 200_000
+    lens = O.zipf_lengths(n, s=1.1)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    host = O.synth_fill_np(total)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
+
+
+def test_mixed_golden_digest(W, golden):
+    lens = np.array([1 + (i * 7919) % 1456 for i in range(2048)], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    out = u32_out(2048)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), 2048, out)
+    got = to_u32(out, 2048)
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == golden["mixed_2048"]["sha256_le_u32"]
+
+
+def test_var_shuffled_offsets_and_empty(W):
+    rng = np.random.default_rng(5)
+    n = 5000
+    lens = rng.integers(0, 1485, n).astype(np.uint32)
+    lens[::17] = 0
+    total = 3_000_000
+    offs = rng.integers(0, total - 1500, n).astype(np.uint64)  # overlapping, unordered
+    host = O.synth_fill_np(total, start_byte=99)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
+
+
+def test_var_bad_length_sets_status(W):
+    W.device_status(0, clear=True)
+    host = O.synth_fill_np(10000)
+    d = dev_u8(host)
+    offs = torch.tensor([0, 10], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([5000, 20], dtype=torch.int32, device="cuda")
+    out = u32_out(2)
+    W.crc32_batch_var(d, 10000, offs, lens, 2, out)
+    got = to_u32(out, 2)
+    assert got[0] == 0 and got[1] == O.crc32(host[10:30])
+    assert W.device_status(0, clear=True) & 1
+
+
+# ---- receiver verify, packet builder, host pipelines -----------------------------------
+def _datagrams(n, stride, rng):
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    rl = np.zeros(n, dtype=np.uint32)
+    payloads = []
+    for i in range(n):
+        L = int(rng.integers(0, min(stride - 16, 1484) + 1))
+        p = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        dg = O.build_datagram(i, p)
+        buf[i * stride:i * stride + len(dg)] = np.frombuffer(dg, dtype=np.uint8)
+        rl[i] = len(dg)
+        payloads.append(p)
+    return buf, rl
+
+
+def test_verify_batch(W):
+    rng = np.random.default_rng(3)
+    n, stride = 3000, 1500
+    buf, rl = _datagrams(n, stride, rng)
+    # corrupt: payload bit flips, header checksum flips, runts, recv_len > stride
+    flip = rng.choice(n, 300, replace=False)
+    for i in flip[:200]:
+        if rl[i] > 16:
+            buf[i * stride + 16 + int(rng.integers(0, rl[i] - 16))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    for i in flip[200:250]:
+        buf[i * stride + 12] ^= 0x80
+    rl[flip[250:270]] = rng.integers(0, 16, 20).astype(np.uint32)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    d = dev_u8(buf)
+    r = torch.from_numpy(rl.view(np.int32)).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    crc = u32_out(n)
+    W.verify_batch(d, stride, r, n, ok, crc)
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), want_ok)
+    assert np.array_equal(to_u32(crc, n), want_crc)
+    assert want_ok.sum() < n - 200  # the corruptions were caught
+
+
+def test_host_verify(W):
+    rng = np.random.default_rng(4)
+    n, stride = 500, 1472
+    buf, rl = _datagrams(n, stride, rng)
+    buf[5 * stride + 30] ^= 4
+    ok, crc = W.host_verify(buf, stride, rl)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    assert np.array_equal(ok, want_ok) and np.array_equal(crc, want_crc)
+
+
+def test_build_data_packets(W):
+    for total in (64, 1456, 2216, 10202, 1456 * 300 + 17):
+        host = O.synth_fill_np(total, start_byte=total)
+        d = dev_u8(np.concatenate([host, np.zeros(16, np.uint8)]))
+        nch = (total + 1455) // 1456
+        wire = torch.zeros(nch * 1472, dtype=torch.uint8, device="cuda")
+        wl = u32_out(nch)
+        W.build_data_packets(d, total, 7, wire, 1472, wl)
+        torch.cuda.synchronize()
+        w = wire.cpu().numpy()
+        lens = to_u32(wl, nch)
+        for i in range(nch):
+            p = host[i * 1456:(i + 1) * 1456].tobytes()
+            want = O.build_datagram(7 + i, p)
+            assert lens[i] == len(want)
+            assert w[i * 1472:i * 1472 + len(want)].tobytes() == want, (total, i)
+
+
+def test_host_chunked_pageable_and_pinned(W):
+    nbytes = 40 * (1 << 20) + 64  # crosses slab boundaries? (64 MiB slabs) keep moderate
+    host = O.synth_fill_np(nbytes, start_byte=5)
+    got = W.host_chunked(host, 1456)
+    want = O.batch_fixed(np.concatenate([host, np.zeros(1456, np.uint8)]), 1456, 1456, got.size - 1, threads=8)
+    assert np.array_equal(got[:-1], want)
+    assert got[-1] == O.crc32(host[(got.size - 1) * 1456:])
+    pb = W.PinnedBuffer(nbytes)
+    pb.array[:] = host
+    got2 = W.host_chunked(pb.array, 1456)
+    assert np.array_equal(got2, got)
+    pb.free()
+
+
+def test_host_chunked_multi_slab(W):
+    nbytes = 150 * (1 << 20) + 1000  # > 2 slabs of 64 MiB
+    host = O.synth_fill_np(nbytes, start_byte=1)
+    got = W.host_chunked(host, 1456)
+    n = got.size
+    idx = np.r_[0:50, n // 2 - 25:n // 2 + 25, n - 50:n]
+    for i in idx:
+        assert got[i] == O.crc32(host[i * 1456:(i + 1) * 1456]), i
+
+
+def test_host_batch_fixed_odd_stride(W):
+    host = O.synth_fill_np(1001 * 999 + 10)
+    got = W.host_batch_fixed(host, 1001, 999, 999)
+    assert np.array_equal(got, O.batch_fixed(host, 1001, 999, 999))
+
+
+# ---- full target size through properties ------------------------------------------------
+def test_target_1m_properties(W):
+    n = 1 << 20
+    buf = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    fast = u32_out(n)
+    W.crc32_batch_fixed(buf, 1456, 1456, n, fast)  # braided kernel
+    # general kernel on the same bytes through the var entry (different algorithm)
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * 1456
+    lens = torch.full((n,), 1456, dtype=torch.int32, device="cuda")
+    gen = u32_out(n)
+    W.crc32_batch_var(buf, n * 1456, offs, lens, n, gen)
+    a, b = to_u32(fast, n), to_u32(gen, n)
+    assert np.array_equal(a, b)
+    rng = np.random.default_rng(1)
+    for i in np.r_[0, 1, n - 1, rng.integers(0, n, 200)]:
+        pkt = O.synth_fill_np(1456, start_byte=int(i) * 1456)
+        assert a[i] == O.crc32(pkt), i
+    # idempotence: a second launch gives the same bytes
+    W.crc32_batch_fixed(buf, 1456, 1456, n, fast)
+    assert np.array_equal(to_u32(fast, n), a)
+
+
+def test_errors_are_loud(W):
+    out = u32_out(4)
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(W.WtpError):
+        W.crc32_batch_fixed(buf, 8192, 8192, 4, out)
+    with pytest.raises(W.WtpError):
+        W.verify_batch(buf, 8, torch.zeros(4, dtype=torch.int32, device="cuda"), 4,
+                       torch.zeros(4, dtype=torch.uint8, device="cuda"))

@@ -1,0 +1,47 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests -> bench -> rocprofv3 kernel-trace stats.
+# Every GPU step has its own time limit; a crash-type exit (fault, abort, segfault,
+# time limit) ends the script without starting further GPU work.
+#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG="${1:-run}"; shift || true
+STEPS="${*:-tests bench prof}"
+OUT="gpurun_out/$TAG"
+mkdir -p "$OUT"
+ROOT="$(pwd)"
+
+fatal() {  # exit codes that mean the GPU step crashed or hung
+  case "$1" in 0|1|2|5) return 1 ;; *) return 0 ;; esac
+}
+
+run() {  # run <name> <seconds> <cmd...>
+  local name="$1" secs="$2"; shift 2
+  echo "[$(date +%T)] start $name" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] end $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -n 5 "$OUT/$name.log"
+  if fatal "$rc"; then echo "FATAL rc=$rc in $name; stopping" | tee -a "$OUT/steps.log"; exit "$rc"; fi
+  return 0
+}
+
+rocminfo 2>/dev/null | grep -m3 -E "Marketing Name|gfx950" > "$OUT/device.txt" || true
+nproc > "$OUT/host_cpus.txt"; lscpu 2>/dev/null | grep -m1 "Model name" >> "$OUT/host_cpus.txt" || true
+
+for s in $STEPS; do
+  case "$s" in
+    tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf --timeout=600 ;;
+    bench) run bench 400 python bench.py --steps 50 --warmup 5 ;;
+    prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline
+           cd "$ROOT" ;;
+    pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$ROOT/$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
+           cd "$ROOT" ;;
+    extra) run extra 600 python tools/bench_configs.py --out "$OUT/configs.json" ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+  esac
+done
+echo "done" | tee -a "$OUT/steps.log"
