@@ -37,11 +37,11 @@ METRIC = "GiB/s CRC-32 over device-resident 1456-B payloads; % of HBM read roofl
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--packets-per-rank", type=int, default=1 << 20)
-    ap.add_argument("--cpu-seconds", type=float, default=4.0,
-                    help="target wall seconds of each CPU-baseline leg (1 thread, all threads)")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0,
+                    help="target wall seconds of the 1-thread CPU-baseline leg (the all-thread leg runs 1/3 of it)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL gather inside the step")
@@ -77,10 +77,11 @@ def cpu_baseline(n_sample: int, seconds: float, threads: int) -> dict:
     for nt in (1, threads):
         run(nt)  # warm
         done, t0 = 0.0, time.perf_counter()
+        budget = seconds if nt == 1 else seconds / 3
         while True:
             done += run(nt)
             el = time.perf_counter() - t0
-            if el >= seconds:
+            if el >= budget:
                 break
         res[nt] = (done / el / 2**30, done, el)
     # sanity: the baseline computes the same CRCs as the oracle
@@ -88,7 +89,7 @@ def cpu_baseline(n_sample: int, seconds: float, threads: int) -> dict:
     v1, vn = res[1], res[threads]
     return {
         "value": round(vn[0], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-        "sample": f"{n_sample} x {PAYLOAD} B synthetic packets (seed 0x5EED), looped for ~{seconds:.0f} s per leg; "
+        "sample": f"{n_sample} x {PAYLOAD} B synthetic packets (seed 0x5EED), looped ~{seconds:.0f} s on 1 thread and ~{seconds/3:.0f} s on {threads}; "
                   f"{kind} = {'cpp/src/common/Crc32.hpp:91-102 compiled -O2 (oracle/_ref)' if ref else 'oracle/crc32_oracle.c'}",
         "value_1core": round(v1[0], 4),
         "cpu_seconds": round(v1[2] + vn[2] * threads, 1),

@@ -83,7 +83,7 @@ uint32_t wtp_crc32(const void *buf, size_t size);
    Sender packet build, batched: payload i = d_payloads[i*stride .. i*stride+len).
    Replaces the per-chunk crc32 of Packet(DATA, chunk, seq) in the send loop
    (cpp/src/base/Sender.cpp:88-95 -> Packet.cpp:13).  Fast path (braided CDNA4
-   kernel): (base + len) % 16 == 0, stride % 16 == 0, 16 <= len <= 1456, len % 16 == 0;
+   kernel): base % 16 == 0, stride % 16 == 0, len % 16 == 0, 16 <= len <= 1536;
    other shapes run the general kernel. */
 int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, size_t n,
                           uint32_t *d_out, void *stream);

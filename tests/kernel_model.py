@@ -49,11 +49,28 @@ class Tables:
         return O.shift(0xFFFFFFFF, L) ^ 0xFFFFFFFF
 
 
-def braid_crc(T: Tables, pkt: bytes) -> int:
-    """k_fixed_braid for one packet (len % 16 == 0, 16 <= len <= 1536)."""
+def frame_start(st: int, L: int, rows: int) -> int:
+    """Frame placement of k_fixed_braid: 128-B aligned if the frame still covers the
+    packet end, else 64-B aligned, else right-aligned to the packet end."""
+    frame = 256 * rows
+    en = st + L
+    for a in (128, 64):
+        fs = st - st % a
+        if fs + frame >= en:
+            return fs
+    return en - frame
+
+
+def braid_crc(T: Tables, pkt: bytes, addr: int = 0) -> int:
+    """k_fixed_braid for one packet (len % 16 == 0, 16 <= len <= 1536) starting at
+    device address `addr` (16-B aligned)."""
     L = len(pkt)
     rows = (L + 255) // 256
-    frame = b"\0" * (rows * 256 - L) + pkt
+    fs = frame_start(addr, L, rows)
+    lead = addr - fs
+    trail = fs + rows * 256 - (addr + L)  # T: zero bytes after the packet, undone below
+    frame = b"\0" * lead + pkt + b"\0" * trail
+    assert len(frame) == rows * 256
     B = [[0, 0, 0, 0] for _ in range(G)]
     for i in range(rows):
         for j in range(G):
@@ -72,7 +89,12 @@ def braid_crc(T: Tables, pkt: bytes) -> int:
                 nv[j] = v[j] ^ _apply(T.inv[16 * d], u)
         v = nv
         d *= 2
-    return v[0] ^ T.init_const(L)
+    r = v[0]
+    t = trail // 16
+    for bit, n in ((1, 16), (2, 32), (4, 64), (8, 128)):
+        if t & bit:
+            r = _apply(T.inv[n], r)
+    return r ^ T.init_const(L)
 
 
 def pieces_crc(T: Tables, buf: bytes, off: int, L: int) -> int:

@@ -311,3 +311,15 @@ def test_errors_are_loud(W):
     with pytest.raises(W.WtpError):
         W.verify_batch(buf, 8, torch.zeros(4, dtype=torch.int32, device="cuda"), 4,
                        torch.zeros(4, dtype=torch.uint8, device="cuda"))
+
+
+@pytest.mark.parametrize("lead", [16, 32, 48, 64, 80, 96, 112])
+def test_fast_path_frame_placements(W, lead):
+    # every 16-B base offset modulo 128 exercises a different braid frame placement
+    for L, stride in ((1456, 1456), (1456, 1472), (256, 272), (1536, 1536), (16, 16), (1296, 1312)):
+        n = 333
+        host = O.synth_fill_np(lead + n * stride + 16, start_byte=lead + L)
+        d = dev_u8(host)
+        out = u32_out(n)
+        W.crc32_batch_fixed(d[lead:], stride, L, n, out)
+        assert np.array_equal(to_u32(out, n), O.batch_fixed(host[lead:], stride, L, n)), (L, stride)

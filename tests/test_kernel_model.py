@@ -15,7 +15,8 @@ def T():
 def test_braid_model(T, L):
     for seed_off in (0, 77777):
         pkt = O.synth_fill_np(L, start_byte=seed_off + L).tobytes()
-        assert braid_crc(T, pkt) == O.crc32(pkt), L
+        for addr in range(0, 256, 16):  # every frame placement case
+            assert braid_crc(T, pkt, addr) == O.crc32(pkt), (L, addr)
 
 
 @pytest.mark.parametrize("L", [0, 1, 3, 4, 5, 63, 64, 65, 127, 128, 129, 700, 1455, 1456, 1484, 4096])

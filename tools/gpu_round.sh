@@ -8,9 +8,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG="${1:-run}"; shift || true
 STEPS="${*:-tests bench prof}"
-OUT="gpurun_out/$TAG"
-mkdir -p "$OUT"
 ROOT="$(pwd)"
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
 
 fatal() {  # exit codes that mean the GPU step crashed or hung
   case "$1" in 0|1|2|5) return 1 ;; *) return 0 ;; esac
@@ -33,12 +33,12 @@ nproc > "$OUT/host_cpus.txt"; lscpu 2>/dev/null | grep -m1 "Model name" >> "$OUT
 for s in $STEPS; do
   case "$s" in
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf --timeout=600 ;;
-    bench) run bench 400 python bench.py --steps 50 --warmup 5 ;;
+    bench) run bench 400 python bench.py ;;
     prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline
+             -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline
            cd "$ROOT" ;;
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-             -d "$ROOT/$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
+             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
            cd "$ROOT" ;;
     extra) run extra 600 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -1,0 +1,313 @@
+// kbench.hip — standalone kernel ablation harness (diagnostics only, not the product).
+// Builds against the product kernel source and times, in one process with interleaved
+// rounds (guide §5.4 rule 24):
+//   read_probe   : the HBM read ceiling of this access shape (dwordx4 nt loads + XOR)
+//   braid        : the production k_fixed_braid<6>
+//   braid_nolut  : same loads/loop, table lookups replaced by XOR (memory + VALU only)
+//   braid_nocomb : production lookups, the x^-k folds and cross-lane tree removed
+// Output: one line per variant with median/min time and GB/s on 1M x 1456 B.
+#include "../a3-reliable-transport_amd/csrc/crc32_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+#include <functional>
+#include <cstring>
+#include <unistd.h>
+
+using namespace wtp;
+using namespace wtp::dev;
+
+__global__ __launch_bounds__(1024) void k_read_probe(const u32x4 *__restrict__ p, uint64_t n16, uint32_t *out) {
+    uint32_t acc = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
+        u32x4 v = __builtin_nontemporal_load(p + i);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// MODE bit0: no table lookups; bit1: no combine
+template <int ROWS, int MODE>
+__global__ __launch_bounds__(1024) void k_braid_diag(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+                                                     uint64_t n, uint32_t *__restrict__ out,
+                                                     const uint32_t *__restrict__ gtab, uint32_t cinit) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    fill_replicated(lds, gtab + OFF_BRAID);
+    fill_ops(lds, gtab + OFF_INV, 6);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint32_t j = lane & (kG - 1), q = lane >> 4;
+    const RepKeys K(lane);
+    constexpr uint32_t kFrame = 256u * ROWS;
+    const uint32_t zc = (kFrame - len) >> 4;
+    const uint64_t rounds = (n + 3) >> 2;
+    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    auto load_round = [&](uint64_t rr, u32x4 (&w)[ROWS]) {
+        uint64_t p = rr * 4 + q;
+        p = p < n ? p : n - 1;
+        const uint8_t *fs = base + p * stride + len - kFrame;
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) {
+            const uint32_t c = uint32_t(i) * kG + j;
+            if (c >= zc) w[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + c * 16u));
+            else w[i] = u32x4{0, 0, 0, 0};
+        }
+    };
+    u32x4 nxt[ROWS];
+    if (r < rounds) load_round(r, nxt);
+    for (; r < rounds; r += rstep) {
+        u32x4 w[ROWS];
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) w[i] = nxt[i];
+        if (r + rstep < rounds) load_round(r + rstep, nxt);
+        uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#pragma unroll
+        for (int i = 0; i < ROWS; ++i) {
+            if (MODE & 1) {
+                b0 = (b0 ^ w[i].x) * 3u; b1 = (b1 ^ w[i].y) * 3u; b2 = (b2 ^ w[i].z) * 3u; b3 = (b3 ^ w[i].w) * 3u;
+            } else {
+                b0 = rep_word(lds, K, b0 ^ w[i].x);
+                b1 = rep_word(lds, K, b1 ^ w[i].y);
+                b2 = rep_word(lds, K, b2 ^ w[i].z);
+                b3 = rep_word(lds, K, b3 ^ w[i].w);
+            }
+        }
+        uint32_t v;
+        if (MODE & 2) {
+            v = b0 ^ b1 ^ b2 ^ b3;
+        } else {
+            v = b0 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b1) ^
+                op_apply(lds, kRepBytes + 1 * kOpBytes, b2 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b3));
+#pragma unroll
+            for (uint32_t d = 1, o = 2; d < kG; d <<= 1, ++o) {
+                const uint32_t u = __shfl_down(v, d, kG);
+                if ((j & (2 * d - 1)) == 0) v ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
+            }
+        }
+        const uint64_t p = r * 4 + q;
+        if (j == 0 && p < n) out[p] = v ^ cinit;
+    }
+}
+
+// Same load pattern as the braid (16 lanes x 16 B per packet row, 4 packets/wave),
+// no compute: isolates the access-pattern cost.  NT: nontemporal loads.
+template <int ROWS, bool NT, int DEPTH>
+__global__ __launch_bounds__(1024) void k_strided_probe(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+                                                        uint64_t n, uint32_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint32_t j = lane & 15u, q = lane >> 4;
+    constexpr uint32_t kFrame = 256u * ROWS;
+    const uint32_t zc = (kFrame - len) >> 4;
+    const uint64_t rounds = (n + 3) >> 2;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    uint32_t acc = 0;
+    for (uint64_t r = uint64_t(blockIdx.x) * nwave + wave; r < rounds; r += rstep * DEPTH) {
+        u32x4 w[DEPTH][ROWS];
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd) {
+            uint64_t p = (r + dd * rstep) * 4 + q;
+            p = p < n ? p : n - 1;
+            const uint8_t *fs = base + p * stride + len - kFrame;
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) {
+                const uint32_t c = uint32_t(i) * 16u + j;
+                if (c >= zc) w[dd][i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + c * 16u))
+                                           : *reinterpret_cast<const u32x4 *>(fs + c * 16u);
+                else w[dd][i] = u32x4{0, 0, 0, 0};
+            }
+        }
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd)
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) acc ^= w[dd][i].x ^ w[dd][i].y ^ w[dd][i].z ^ w[dd][i].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// One packet per wave: 64 lanes x 16 B = 1 KiB contiguous rows (G = 64 layout), no compute.
+template <int DEPTH>
+__global__ __launch_bounds__(1024) void k_g64_probe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    uint32_t acc = 0;
+    for (uint64_t p = uint64_t(blockIdx.x) * nwave + wave; p < n; p += rstep * DEPTH) {
+        u32x4 w[DEPTH][2];
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd) {
+            uint64_t pp = p + dd * rstep;
+            pp = pp < n ? pp : n - 1;
+            const uint8_t *fs = base + pp * 1456 + 1456 - 2048;
+            w[dd][0] = lane >= 37 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + lane * 16u)) : u32x4{0,0,0,0};
+            w[dd][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + 1024 + lane * 16u));
+        }
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd) acc ^= w[dd][0].x ^ w[dd][0].w ^ w[dd][1].y ^ w[dd][1].z;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Generic braid-shaped load probe: G lanes x 16 B per packet row, 64/G packets per wave,
+// ROWS rows, DEPTH rounds in flight.  AL=0: frame right-aligned to the packet end (as the
+// production kernel); AL=1: frame start 128-B aligned when it fits, else 64-B aligned.
+template <int G, int ROWS, int AL, int DEPTH, int LDSF = 0>
+__global__ __launch_bounds__(1024) void k_gprobe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out,
+                                                 const uint32_t *__restrict__ gtab = nullptr) {
+    constexpr int PW = 64 / G;
+    // LDSF bit0: allocate + fill the braid kernel's 152 KiB LDS image first; bit1: store 1 u32 per packet
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[(LDSF & 1) ? kLdsWords : 4];
+    if (LDSF & 1) {
+        char *lds = reinterpret_cast<char *>(lds_w);
+        fill_replicated(lds, gtab + OFF_BRAID);
+        fill_ops(lds, gtab + OFF_INV, 6);
+        __syncthreads();
+    }
+    constexpr uint32_t RB = 16u * G, kFrame = RB * ROWS;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint32_t j = lane % G, q = lane / G;
+    const uint64_t rounds = (n + PW - 1) / PW;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    uint32_t acc = 0;
+    for (uint64_t r = uint64_t(blockIdx.x) * nwave + wave; r < rounds; r += rstep * DEPTH) {
+        u32x4 w[DEPTH][ROWS];
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd) {
+            uint64_t p = (r + dd * rstep) * PW + q;
+            p = p < n ? p : n - 1;
+            const uint64_t st = p * 1456, en = st + 1456;
+            uint64_t fs = en - kFrame;
+            if (AL) {
+                const uint64_t a128 = st & ~uint64_t(127), a64 = st & ~uint64_t(63);
+                fs = (a128 + kFrame >= en) ? a128 : a64;
+            }
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) {
+                const uint64_t o = fs + uint64_t(i) * RB + j * 16u;
+                if (o >= st && o < en) w[dd][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + o));
+                else w[dd][i] = u32x4{0, 0, 0, 0};
+            }
+        }
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd)
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) acc ^= w[dd][i].x ^ w[dd][i].y ^ w[dd][i].z ^ w[dd][i].w;
+        if (LDSF & 2) {
+            const uint64_t p = r * PW + q;
+            if (j == 0 && p < n) out[p] = acc ^ ((LDSF & 1) ? lds_w[lane] : 0u);
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc ^ ((LDSF & 1) ? lds_w[lane] : 0u);
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+int main(int argc, char **argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 20);
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const uint64_t bytes = n * 1456;
+    CK(hipSetDevice(0));
+    if (wtp_init(0)) { fprintf(stderr, "init: %s\n", wtp_last_error()); return 1; }
+    DevState &s = g_dev[0];
+    uint8_t *buf; uint32_t *out;
+    CK(hipMalloc(&buf, bytes + 64));
+    CK(hipMalloc(&out, n * 4 + 64));
+    if (wtp_synth_fill(buf, 0, bytes, 0x5EED, nullptr)) return 1;
+    CK(hipDeviceSynchronize());
+    const uint32_t cinit = init_const(1456);
+    const uint64_t rounds = (n + 3) / 4;
+    const unsigned grid = unsigned(std::min<uint64_t>((rounds + 15) / 16, s.cus));
+
+    struct V { const char *name; std::function<void()> f; std::vector<float> t; };
+    std::vector<V> vs;
+    vs.push_back({"read_probe_g256x1024", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(1024), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
+    vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
+    vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
+    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f0_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f1_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_old_rightaligned", [&] { hipLaunchKernelGGL((k_braid_diag<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_nolut", [&] { hipLaunchKernelGGL((k_braid_diag<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_nolut_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
+    vs.push_back({"strided_nt_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
+    vs.push_back({"strided_plain_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, false, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
+    vs.push_back({"strided_nt_d2_g512", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(512), dim3(512), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
+    vs.push_back({"g64_d2", [&] { hipLaunchKernelGGL((k_g64_probe<2>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
+    vs.push_back({"g64_d4", [&] { hipLaunchKernelGGL((k_g64_probe<4>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
+    vs.push_back({"g64_d4_g1024x256", [&] { hipLaunchKernelGGL((k_g64_probe<4>), dim3(1024), dim3(256), 0, 0, buf, n, out); }, {}});
+#define GP(G, R, AL, D, GR, BL) vs.push_back({"gprobe_G" #G "_R" #R "_al" #AL "_d" #D "_" #GR "x" #BL, [&] { hipLaunchKernelGGL((k_gprobe<G, R, AL, D>), dim3(GR), dim3(BL), 0, 0, buf, n, out); }, {}})
+    GP(16, 6, 0, 1, 256, 1024); GP(16, 6, 1, 1, 256, 1024); GP(16, 6, 0, 2, 256, 1024); GP(16, 6, 1, 2, 256, 1024);
+    GP(8, 12, 0, 1, 256, 1024); GP(8, 12, 1, 1, 256, 1024); GP(8, 12, 1, 2, 256, 1024);
+    GP(32, 3, 0, 2, 256, 1024); GP(32, 3, 1, 2, 256, 1024); GP(32, 3, 1, 4, 256, 1024);
+    GP(16, 6, 1, 2, 512, 512); GP(8, 12, 1, 1, 512, 512);
+#define GPL(G, R, AL, D, F) vs.push_back({"gprobe_G" #G "_R" #R "_al" #AL "_d" #D "_ldsf" #F, [&] { hipLaunchKernelGGL((k_gprobe<G, R, AL, D, F>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out, s.tabs); }, {}})
+    GPL(16, 6, 1, 1, 1); GPL(16, 6, 1, 1, 2); GPL(16, 6, 1, 1, 3); GPL(16, 6, 0, 1, 3);
+    vs.push_back({"pieces_fixed", [&] {  // general kernel, fixed provider
+        launch_pieces(s, buf, bytes, dev::FixedProvL{1456, 0, 1456u}, n, dev::CrcEpi{out}, nullptr); }, {}});
+
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    for (auto &v : vs) { v.f(); v.f(); }
+    CK(hipDeviceSynchronize());
+    for (int r = 0; r < reps; ++r)
+        for (auto &v : vs) {
+            CK(hipEventRecord(a, 0));
+            v.f();
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms; CK(hipEventElapsedTime(&ms, a, b));
+            v.t.push_back(ms);
+        }
+    // sustained: 200 back-to-back launches per selected variant (DVFS steady state)
+    if (getenv("KB_SUSTAIN")) {
+        const int NS = 200;
+        std::vector<hipEvent_t> ev(NS + 1);
+        for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
+        for (auto &v : vs) {
+            if (!strstr(getenv("KB_SUSTAIN"), v.name) && strcmp(getenv("KB_SUSTAIN"), "all")) continue;
+            CK(hipDeviceSynchronize());
+            usleep(200000);  // let clocks settle between variants
+            CK(hipEventRecord(ev[0], 0));
+            for (int r = 0; r < NS; ++r) { v.f(); CK(hipEventRecord(ev[r + 1], 0)); }
+            CK(hipDeviceSynchronize());
+            std::vector<float> t;
+            for (int r = 0; r < NS; ++r) { float ms; CK(hipEventElapsedTime(&ms, ev[r], ev[r + 1])); t.push_back(ms); }
+            std::vector<float> tail(t.begin() + NS / 2, t.end());
+            std::sort(tail.begin(), tail.end());
+            float tot; CK(hipEventElapsedTime(&tot, ev[0], ev[NS]));
+            printf("SUSTAIN %-26s all %.1f GB/s | steady median %.4f ms %.1f GB/s | t[0..]=", v.name, bytes * NS / (tot * 1e-3) / 1e9,
+                   tail[tail.size() / 2], bytes / (tail[tail.size() / 2] * 1e-3) / 1e9);
+            for (int r = 0; r < NS; r += 20) printf("%.0f ", t[r] * 1000);
+            printf("us\n");
+        }
+    }
+    // back-to-back launches of the production kernel (as bench.py issues them)
+    {
+        std::vector<hipEvent_t> ev(2 * reps);
+        for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(ev[2 * r], 0));
+            vs[3].f();
+            CK(hipEventRecord(ev[2 * r + 1], 0));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<float> t;
+        for (int r = 0; r < reps; ++r) { float ms; CK(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1])); t.push_back(ms); }
+        std::sort(t.begin(), t.end());
+        printf("braid_prod back-to-back: median %.4f ms (%.1f GB/s) min %.4f max %.4f\n", t[t.size() / 2],
+               bytes / (t[t.size() / 2] * 1e-3) / 1e9, t[0], t.back());
+    }
+    printf("# n=%llu packets x 1456 B = %.3f GB per launch, grid(braid)=%u, reps=%d\n", (unsigned long long)n, bytes / 1e9, grid, reps);
+    for (auto &v : vs) {
+        std::sort(v.t.begin(), v.t.end());
+        const float med = v.t[v.t.size() / 2], mn = v.t[0];
+        printf("%-24s median %.4f ms (%.1f GB/s, %.1f%% of 8 TB/s)  min %.4f ms (%.1f GB/s)\n", v.name, med,
+               bytes / (med * 1e-3) / 1e9, 100.0 * bytes / (med * 1e-3) / 8e12, mn, bytes / (mn * 1e-3) / 1e9);
+    }
+    return 0;
+}
