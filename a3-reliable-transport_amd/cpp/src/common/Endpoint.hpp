@@ -1,0 +1,133 @@
+// Endpoint.hpp — shared plumbing of the WTP endpoints (wSender / wReceiver): argument
+// parsing for the spec'd flags (README.md:83-89, 120-125), the per-packet log line
+// `<type> <seqNum> <length> <checksum>` (README.md:93-99), UDP sockets, and the checksum
+// engine that routes whole batches to the MI355X library (--crc gpu) or to the CPU
+// crc32() of Crc32.hpp (--crc cpu, the reference's behaviour).
+#pragma once
+
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "Crc32.hpp"
+#include "PacketHeader.hpp"
+
+namespace wtp {
+
+struct Args {
+    std::map<std::string, std::string> kv;
+    Args(int argc, char **argv, const std::map<std::string, std::string> &alias) {
+        for (int i = 1; i < argc; ++i) {
+            std::string k = argv[i];
+            auto it = alias.find(k);
+            if (it == alias.end()) throw std::runtime_error("unknown argument " + k);
+            if (it->second.rfind("flag:", 0) == 0) {
+                kv[it->second.substr(5)] = "1";
+                continue;
+            }
+            if (i + 1 >= argc) throw std::runtime_error("missing value for " + k);
+            kv[it->second] = argv[++i];
+        }
+    }
+    std::string get(const std::string &k, const std::string &def = "") const {
+        auto it = kv.find(k);
+        return it == kv.end() ? def : it->second;
+    }
+    bool has(const std::string &k) const { return kv.count(k) != 0; }
+};
+
+class Log {
+   public:
+    explicit Log(const std::string &path) : f_(path.empty() ? nullptr : std::fopen(path.c_str(), "w")) {}
+    ~Log() {
+        if (f_) std::fclose(f_);
+    }
+    void pkt(const PacketHeader &h) {
+        if (f_) {
+            std::fprintf(f_, "%u %u %u %u\n", h.type, h.seqNum, h.length, h.checksum);
+            std::fflush(f_);
+        }
+    }
+
+   private:
+    FILE *f_;
+};
+
+// Checksums for whole batches.  GPU mode goes through the C-ABI; CPU mode is the
+// reference's one-call-per-packet crc32().
+class Checksums {
+   public:
+    explicit Checksums(const std::string &mode) : gpu_(mode == "gpu") {
+        if (mode != "gpu" && mode != "cpu") throw std::runtime_error("--crc must be cpu or gpu");
+        if (gpu_ && wtp_init(0) != WTP_OK) throw std::runtime_error(std::string("GPU CRC unavailable: ") + wtp_last_error());
+    }
+    bool gpu() const { return gpu_; }
+
+    // Sender build: crc of every kMaxPayload chunk of the file (Sender.cpp:88-92).
+    std::vector<uint32_t> chunks(const uint8_t *buf, size_t n) const {
+        const size_t nch = (n + kMaxPayload - 1) / kMaxPayload;
+        std::vector<uint32_t> out(nch);
+        if (!nch) return out;
+        if (gpu_) {
+            if (wtp_crc32_host_chunked(buf, n, kMaxPayload, out.data()) != WTP_OK)
+                throw std::runtime_error(std::string("wtp_crc32_host_chunked: ") + wtp_last_error());
+        } else {
+            for (size_t i = 0; i < nch; ++i) out[i] = crc32(buf + i * kMaxPayload, std::min(kMaxPayload, n - i * kMaxPayload));
+        }
+        return out;
+    }
+
+    // Receiver verify (Receiver.cpp:203-206): CRC over datagram bytes [16, len).
+    bool verify(const uint8_t *dgram, size_t len) const {
+        if (len < kHeaderBytes) return false;
+        if (gpu_) {
+            uint32_t rl = uint32_t(len), crc = 0;
+            uint8_t ok = 0;
+            if (wtp_crc32_host_verify(dgram, len, &rl, 1, &ok, &crc) != WTP_OK)
+                throw std::runtime_error(std::string("wtp_crc32_host_verify: ") + wtp_last_error());
+            return ok != 0;
+        }
+        return get_header(dgram).checksum == crc32(dgram + kHeaderBytes, len - kHeaderBytes);
+    }
+
+   private:
+    bool gpu_;
+};
+
+inline int udp_socket() {
+    int fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+    if (fd < 0) throw std::runtime_error("socket() failed");
+    return fd;
+}
+
+inline void set_rcv_timeout_ms(int fd, int ms) {
+    timeval tv{ms / 1000, (ms % 1000) * 1000};
+    if (setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv) < 0) throw std::runtime_error("setsockopt failed");
+}
+
+inline sockaddr_in addr_of(const std::string &host, int port) {
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(uint16_t(port));
+    if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) throw std::runtime_error("bad IPv4 address " + host);
+    return a;
+}
+
+// Build one datagram (header htonl'd, Packet.cpp:40-47 / Sender.cpp:189-194).
+inline size_t make_datagram(uint8_t *wire, uint32_t type, uint32_t seq, const uint8_t *payload, uint32_t len,
+                            uint32_t checksum) {
+    put_header(wire, PacketHeader{type, seq, len, checksum});
+    if (len) std::memcpy(wire + kHeaderBytes, payload, len);
+    return kHeaderBytes + len;
+}
+
+}  // namespace wtp

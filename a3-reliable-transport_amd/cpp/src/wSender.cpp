@@ -1,0 +1,124 @@
+// wSender.cpp — WTP sender (go-back-N), config C1 plumbing around the CRC path.
+//
+//   wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu]
+//
+// Reference behaviour (mmheyer/a3-reliable-transport README.md:62-127, cpp/src/base/
+// Sender.cpp): START with a random seqNum until ACKed, DATA seqNums from 0 in chunks of
+// 1456 B, cumulative ACKs, a 500 ms timer that resends the whole window when it does not
+// advance, END with the START seqNum until ACKed.
+//
+// The checksum path is the one this repository accelerates: the whole file is read up
+// front (as Sender.cpp:82 does) and every chunk's CRC is computed in ONE batch — on the
+// MI355X through wtp_crc32_host_chunked with --crc gpu, or with the reference's
+// per-packet crc32() with --crc cpu.  Retransmissions reuse the stored header.
+#include <chrono>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+#include <random>
+
+#include "common/Endpoint.hpp"
+
+using namespace wtp;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+struct Conn {
+    int fd;
+    sockaddr_in peer;
+    Log &log;
+
+    void send(const uint8_t *wire, size_t n) {
+        ::sendto(fd, wire, n, 0, reinterpret_cast<const sockaddr *>(&peer), sizeof peer);
+        log.pkt(get_header(wire));
+    }
+    // Returns true and the ACK header if a valid ACK arrived before the socket timeout.
+    bool recv_ack(PacketHeader &h) {
+        uint8_t buf[2048];
+        ssize_t n = ::recvfrom(fd, buf, sizeof buf, 0, nullptr, nullptr);
+        if (n < ssize_t(kHeaderBytes)) return false;
+        h = get_header(buf);
+        // ACKs carry no payload; crc32 of an empty payload is 0 (Sender.cpp:235-237)
+        if (h.type != ACK || h.checksum != crc32(buf + kHeaderBytes, 0)) return false;
+        log.pkt(h);
+        return true;
+    }
+};
+
+// Send a control packet until its ACK (seqNum == seq) arrives.
+bool control(Conn &c, uint32_t type, uint32_t seq, int max_tries) {
+    uint8_t wire[kHeaderBytes];
+    make_datagram(wire, type, seq, nullptr, 0, crc32(nullptr, 0));
+    for (int t = 0; t < max_tries; ++t) {
+        c.send(wire, sizeof wire);
+        const auto deadline = Clock::now() + std::chrono::milliseconds(500);
+        PacketHeader h;
+        while (Clock::now() < deadline) {
+            if (c.recv_ack(h) && h.seqNum == seq) return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    try {
+        Args a(argc, argv, {{"-h", "host"}, {"--hostname", "host"}, {"-p", "port"}, {"--port", "port"},
+                            {"-w", "window"}, {"--window-size", "window"}, {"-i", "input"}, {"--input-file", "input"},
+                            {"-o", "log"}, {"--output-log", "log"}, {"--crc", "crc"}});
+        const int port = std::stoi(a.get("port", "0"));
+        const int window = std::stoi(a.get("window", "0"));
+        if (port <= 0 || port > 65535 || window <= 0 || !a.has("host") || !a.has("input")) {
+            std::cerr << "usage: wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu]\n";
+            return 1;
+        }
+        Checksums crc(a.get("crc", "cpu"));
+        Log log(a.get("log"));
+
+        std::ifstream in(a.get("input"), std::ios::binary);
+        if (!in) throw std::runtime_error("cannot open " + a.get("input"));
+        std::vector<uint8_t> file((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+
+        // Every DATA checksum in one batch (the device path when --crc gpu).
+        const std::vector<uint32_t> sums = crc.chunks(file.data(), file.size());
+        const uint32_t nchunks = uint32_t(sums.size());
+
+        Conn c{udp_socket(), addr_of(a.get("host"), port), log};
+        set_rcv_timeout_ms(c.fd, 50);
+
+        std::mt19937 gen(std::random_device{}());
+        const uint32_t start_seq = std::uniform_int_distribution<uint32_t>(1, 0xFFFFFFFFu)(gen);
+        if (!control(c, START, start_seq, 100)) throw std::runtime_error("START was never acknowledged");
+
+        uint8_t wire[kMaxDatagram];
+        auto send_chunk = [&](uint32_t i) {
+            const size_t off = size_t(i) * kMaxPayload;
+            const uint32_t len = uint32_t(std::min(kMaxPayload, file.size() - off));
+            c.send(wire, make_datagram(wire, DATA, i, file.data() + off, len, sums[i]));
+        };
+
+        uint32_t base = 0, next = 0;  // window = [base, next)
+        auto timer = Clock::now();
+        while (base < nchunks) {
+            while (next < nchunks && next - base < uint32_t(window)) send_chunk(next++);
+            PacketHeader h;
+            if (c.recv_ack(h) && h.seqNum > base && h.seqNum <= next) {  // cumulative ACK
+                base = h.seqNum;
+                timer = Clock::now();
+            } else if (Clock::now() - timer >= std::chrono::milliseconds(500)) {
+                for (uint32_t s = base; s < next; ++s) send_chunk(s);  // go-back-N
+                timer = Clock::now();
+            }
+        }
+        if (!control(c, END, start_seq, 100)) throw std::runtime_error("END was never acknowledged");
+        ::close(c.fd);
+        std::cout << "sent " << file.size() << " bytes in " << nchunks << " DATA packets (crc " << (crc.gpu() ? "gpu" : "cpu")
+                  << ")\n";
+        return 0;
+    } catch (const std::exception &e) {
+        std::cerr << "wSender: " << e.what() << "\n";
+        return 1;
+    }
+}

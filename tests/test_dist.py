@@ -1,0 +1,77 @@
+"""N > 1 path on CPU: block partition of packets across ranks + gather of the 32-bit
+results to rank 0 (a3-reliable-transport_amd/shard.py), world_size 2 and 4 with gloo.
+Each rank checksums its own contiguous shard of the global synthetic stream (the same
+global byte offsets bench.py uses) — here with the CPU oracle, on the GPU box with the
+HIP kernel — and rank 0 compares the gathered vector with the single-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import shard
+
+PAYLOAD = 1456
+
+
+def test_shard_ranges_cover_disjoint():
+    for n in (0, 1, 7, 1000, 1 << 20, 16_777_216):
+        for world in (1, 2, 3, 4, 8):
+            got = [shard.shard_range(r, world, n) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            for (a, b), (c, d) in zip(got, got[1:]):
+                assert b == c and a <= b
+            sizes = [b - a for a, b in got]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_range(2, 2, 10)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd"), os.path.join(here, "..", "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    import shard as S
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = S.shard_range(rank, world, n_total)
+    shard_bytes = O.synth_fill_np((hi - lo) * PAYLOAD, start_byte=lo * PAYLOAD)
+    local = O.batch_fixed(shard_bytes, PAYLOAD, PAYLOAD, hi - lo)
+    t = torch.from_numpy(local.view(np.int32).copy())
+    full = S.gather_crcs(t, world, rank)
+    if rank == 0:
+        q.put(full.numpy().view(np.uint32).copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_matches_single_process(world):
+    import torch.multiprocessing as mp
+    n_total = 512 * world  # equal shards (gather of equal-length tensors)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import oracle as O
+    want = O.batch_fixed(O.synth_fill_np(n_total * PAYLOAD), PAYLOAD, PAYLOAD, n_total)
+    assert np.array_equal(got, want)

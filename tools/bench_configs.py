@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Measure the non-headline configs of BASELINE.json on one MI355X (writes JSON).
+
+  C2  64K x 1456 B device-resident: single-launch time (launch-bound) + sustained rate
+  C3  1 GiB host file chunked at 1456 B: wtp_crc32_host_chunked end to end, pinned and
+      pageable source (PCIe-bound), plus torch's raw H2D copy rate for reference
+  C5  1 M mixed-length payloads, Zipf(s) on [1,1456] (s = 1.1, 1.0), packed, per-packet
+      offsets/lengths: the general kernel; read bytes = sum(len) + 12 B metadata/packet
+  verify   1 M wire datagrams (stride 1472) through the receiver-verify kernel
+  build    fused DATA packet builder over a 1.4 GiB payload buffer
+Every line carries a spot parity check against the CPU oracle.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "a3-reliable-transport_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import oracle as O  # noqa: E402
+import wtp_crc32 as W  # noqa: E402
+
+GB = 1e9
+GIB = float(1 << 30)
+PEAK = 8000.0
+
+
+def timed(fn, reps, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record()
+    for i in range(reps):
+        fn()
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))
+    tot = ev[0].elapsed_time(ev[reps])
+    return ts[len(ts) // 2], tot / reps
+
+
+def c2():
+    n = 65536
+    buf = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    f = lambda: W.crc32_batch_fixed(buf, 1456, 1456, n, out)  # noqa: E731
+    # single launch from an idle stream
+    singles = []
+    for _ in range(20):
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        f()
+        b.record()
+        torch.cuda.synchronize()
+        singles.append(a.elapsed_time(b))
+    med, mean = timed(f, 500)
+    got = out.cpu().numpy().view(np.uint32)
+    ok = all(int(got[i]) == O.crc32(O.synth_fill_np(1456, start_byte=i * 1456)) for i in (0, n // 3, n - 1))
+    by = n * 1456
+    return {"config": "C2 64K x 1456 B device-resident", "packets": n, "bytes": by,
+            "single_launch_ms_median": round(float(np.median(singles)), 4),
+            "single_launch_GiBps": round(by / (np.median(singles) * 1e-3) / GIB, 1),
+            "sustained_ms_per_launch": round(mean, 4), "sustained_GiBps": round(by / (mean * 1e-3) / GIB, 1),
+            "sustained_frac_hbm": round(by / (mean * 1e-3) / GB / PEAK, 4), "parity_spot": ok}
+
+
+def c3():
+    nbytes = 1 << 30
+    res = {"config": "C3 1 GiB host file -> 1456-B chunks, pinned H2D -> CRC -> D2H, 2 streams", "bytes": nbytes,
+           "chunks": (nbytes + 1455) // 1456}
+    pb = W.PinnedBuffer(nbytes)
+    host = pb.array
+    # fill with the synthetic stream in 64 MiB pieces
+    step = 64 << 20
+    for o in range(0, nbytes, step):
+        host[o:o + step] = O.synth_fill_np(min(step, nbytes - o), start_byte=o)
+    for label, src in (("pinned", host), ("pageable", None)):
+        if src is None:
+            src = np.empty(nbytes, dtype=np.uint8)
+            src[:] = host
+        W.host_chunked(src, 1456)  # warm (allocates the library pipeline)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            crcs = W.host_chunked(src, 1456)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        n = crcs.size
+        ok = all(int(crcs[i]) == O.crc32(host[i * 1456:min((i + 1) * 1456, nbytes)]) for i in (0, n // 2, n - 1))
+        res[label] = {"seconds": round(t, 4), "GiBps": round(nbytes / t / GIB, 2), "GBps": round(nbytes / t / GB, 2),
+                      "parity_spot": ok, "last_chunk_bytes": int(nbytes - (n - 1) * 1456)}
+        del src
+    # raw H2D rate of the link for context
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    ht = torch.from_numpy(host)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d.copy_(ht, non_blocking=True)
+    torch.cuda.synchronize()
+    res["raw_h2d_pinned_GBps"] = round(nbytes / (time.perf_counter() - t0) / GB, 2)
+    pb.free()
+    return res
+
+
+def c5(s):
+    n = 1 << 20
+    lens = O.zipf_lengths(n, s=s)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    d = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d, nbytes=total)
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    f = lambda: W.crc32_batch_var(d, total, do, dl, n, out)  # noqa: E731
+    med, mean = timed(f, 200)
+    got = out.cpu().numpy().view(np.uint32)
+    host = d[:total].cpu().numpy()
+    idx = np.random.default_rng(2).integers(0, n, 2000)
+    ok = bool(np.array_equal(got[idx], O.batch_var(host, offs[idx], lens[idx])))
+    rb = total + 12 * n
+    return {"config": f"C5 1M mixed lengths Zipf(s={s}) on [1,1456], general kernel", "packets": n,
+            "payload_bytes": total, "mean_len": round(total / n, 1), "read_bytes_incl_meta": rb,
+            "ms_per_launch": round(mean, 4), "payload_GiBps": round(total / (mean * 1e-3) / GIB, 1),
+            "read_GBps": round(rb / (mean * 1e-3) / GB, 1), "frac_hbm": round(rb / (mean * 1e-3) / GB / PEAK, 4),
+            "parity_2000_random": ok}
+
+
+def verify():
+    n, stride = 1 << 20, 1472
+    wire = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    payload = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(payload)
+    wl = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    f = lambda: W.verify_batch(wire, stride, wl, n, ok)  # noqa: E731
+    med, mean = timed(f, 100)
+    good = int(ok.sum().item())
+    fb = lambda: W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)  # noqa: E731
+    bmed, bmean = timed(fb, 50)
+    h = wire[:2 * stride].cpu().numpy().tobytes()
+    want = O.build_datagram(0, O.synth_fill_np(1456).tobytes()) + b"\0" * 0
+    return [{"config": "receiver verify, 1M x 1472-B datagrams device-resident", "packets": n,
+             "ms_per_launch": round(mean, 4), "payload_GiBps": round(n * 1456 / (mean * 1e-3) / GIB, 1),
+             "read_GBps": round(n * (stride + 4) / (mean * 1e-3) / GB, 1), "all_ok": good == n},
+            {"config": "fused DATA packet builder, 1M x 1456 B -> 1472-B wire slots", "packets": n,
+             "ms_per_launch": round(bmean, 4), "GBps_read_plus_write": round(n * (1456 + 1472) / (bmean * 1e-3) / GB, 1),
+             "first_datagram_matches_oracle": h[:1472] == want}]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="configs.json")
+    ap.add_argument("--only", default="c2,c3,c5,verify")
+    a = ap.parse_args()
+    assert W.LIB.wtp_init(0) == 0
+    res = {"device": torch.cuda.get_device_name(0), "host_cpus": os.cpu_count(), "results": []}
+    sel = a.only.split(",")
+    if "c2" in sel:
+        res["results"].append(c2())
+    if "c5" in sel:
+        res["results"].append(c5(1.1))
+        res["results"].append(c5(1.0))
+    if "verify" in sel:
+        res["results"].extend(verify())
+    if "c3" in sel:
+        res["results"].append(c3())
+    for r in res["results"]:
+        print(json.dumps(r), flush=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -40,7 +40,7 @@ for s in $STEPS; do
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
              -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
            cd "$ROOT" ;;
-    extra) run extra 600 python tools/bench_configs.py --out "$OUT/configs.json" ;;
+    extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done
