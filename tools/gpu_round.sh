@@ -35,10 +35,10 @@ for s in $STEPS; do
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf --timeout=600 ;;
     bench) run bench 400 python bench.py ;;
     prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline
+             -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline
            cd "$ROOT" ;;
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline
+             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
            cd "$ROOT" ;;
     extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
