@@ -64,11 +64,20 @@ constexpr uint32_t TAB_WORDS = OFF_ZERO + 4;
 // so a ds_read_b32 by lane L always lands in bank L%32 whatever the byte e.
 constexpr uint32_t kRepBytes = 131072;
 constexpr uint32_t kOpBytes = 4096;
-constexpr uint32_t kLdsWords = (kRepBytes + 6 * kOpBytes) / 4;  // 155,648 B
+constexpr uint32_t kLdsWords = (kRepBytes + 6 * kOpBytes) / 4;  // 155,648 B (k_pieces)
+// k_fixed_braid: region A = {braid tables, x^-32}, region B = {x^-64, x^-128} (staggered,
+// conflict-free), then x^-256, x^-512, x^-1024 as plain 4 KiB operators.
+constexpr uint32_t kBraidPlainOps = 131072;
+constexpr uint32_t kBraidLdsWords = (kBraidPlainOps + 3 * kOpBytes) / 4;  // 143,360 B
 
 namespace dev {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Explicit global (address space 1) pointers for the streaming loads: a select between
+// two generic pointers defeats address-space inference and degrades to flat_load, which
+// also counts on lgkmcnt and serialises with the LDS lookups.
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 
 __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
@@ -126,6 +135,53 @@ __device__ __forceinline__ uint32_t op_apply(const char *lds, uint32_t base, uin
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+// ---- staggered 8-copy tables (conflict-free with a quarter of the replication) ------
+// A "table set" is 4 byte-tables (256 u32 each) of one linear map.  Each 32-lane half of
+// a wave is split into 4 groups of 8 lanes; in lookup instruction s, group g reads table
+// (s + g) & 3, so the 4 groups always hit 4 different tables, and copy c = lane & 7 of
+// table t lives in bank 8t + c: all 32 lanes touch distinct banks whatever the bytes.
+// Every lane still XORs one entry of each of the 4 tables, just in a lane-dependent
+// order.  Layout: 256-B rows, one per byte value e; two table sets per 64 KiB region:
+//   byte address = region*65536 + e*256 + set*128 + t*32 + c*4.
+// The per-lane key holds everything but e; v_perm_b32 with a per-lane selector drops the
+// data byte t into bits 8..15, so each lookup is one v_perm + one ds_read_b32 (the set
+// bit is the instruction's immediate offset).
+struct StagKeys {
+    uint32_t kA[4], kB[4], sel[4];
+    __device__ __forceinline__ explicit StagKeys(uint32_t lane) {
+        const uint32_t h = lane & 31u, g = (h >> 3) & 3u, c = h & 7u;
+#pragma unroll
+        for (uint32_t s = 0; s < 4; ++s) {
+            const uint32_t t = (s + g) & 3u;
+            kA[s] = (t << 5) | (c << 2);
+            kB[s] = kA[s] | (1u << 16);
+            sel[s] = 0x0C020000u | ((4u + t) << 8);
+        }
+    }
+};
+
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t stag_apply(const char *lds, const uint32_t (&key)[4], const uint32_t (&sel)[4],
+                                               uint32_t x) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, key[0], sel[0]);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, key[1], sel[1]);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, key[2], sel[2]);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, key[3], sel[3]);
+    return (lds_rd(lds, a0 + OFF) ^ lds_rd(lds, a1 + OFF)) ^ (lds_rd(lds, a2 + OFF) ^ lds_rd(lds, a3 + OFF));
+}
+
+// Fill one table set (1024 words from global: table t at g[256 t]) into the staggered image.
+__device__ __forceinline__ void fill_stag(char *lds, uint32_t region, uint32_t set, const uint32_t *__restrict__ g) {
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+        const uint32_t t = i >> 8, e = i & 255u;
+        const uint32_t v = g[i];
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + region * 65536u + e * 256u + set * 128u + t * 32u);
+        const u32x4 q = {v, v, v, v};
+        dst[0] = q;
+        dst[1] = q;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // 1. braided fixed-length kernel
 // ------------------------------------------------------------------------------------
@@ -137,7 +193,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 // bytes before the packet are free zeros (R_0(0^k || M) = R_0(M)); the T zero bytes
 // after it are undone at the end with x^(-8T) (T/16 < 16: inverse ops 16..128 B).
 constexpr int kBraidFrame = 1;
-constexpr int kBraidDepth = 1;
+constexpr int kBraidDepth = 1;  // rounds of loads kept in flight beyond the one in use
 
 // Bytes of frame before the packet start (st = packet address, 16-B aligned).
 __device__ __forceinline__ uint32_t braid_lead(uintptr_t st, uint32_t len, uint32_t frame) {
@@ -146,57 +202,84 @@ __device__ __forceinline__ uint32_t braid_lead(uintptr_t st, uint32_t len, uint3
 }
 
 // FRAME: 0 = right-aligned to the packet end (no trailing zeros), 1 = 128/64-B aligned
-// start (trailing zeros undone).  DEPTH: rounds of loads in flight per wave (1 or 2).
+// start (trailing zeros undone).
 //
-// Results are not stored per round: on gfx950 stores share vmcnt with loads, so a
-// store per round makes the next round's load wait also wait for the store (-4.3% on
-// the load probe).  Instead the 4 results of each round are shuffled into a collector
-// register (lane 4k + q after k rounds) and every 16 rounds the wave applies the
-// trailing-zero fix x^(-8T) and the init constant to all 64 collected values at once
-// and writes them with one store instruction.
-template <int ROWS, int FRAME = kBraidFrame, int DEPTH = kBraidDepth>
-__global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint64_t stride,
+// The MI355X runs this kernel at its ~1.4 kW board limit (measured: the load-only probe
+// draws ~1.19 kW at 2.39 GHz, this kernel ~1.4 kW at ~2.0 GHz), so every instruction in
+// the loop costs bandwidth.  The loop is kept lean:
+//   - the round's packet base is wave-uniform (SGPRs, scalar multiply); lanes add 32-bit
+//     offsets, so the row loads are `global_load_dwordx4 v, voff, s[base] offset:256*i`;
+//   - only the first and last frame rows can hold bytes outside the packet: they clamp
+//     their offset to the packet start and zero the data at use (v_cndmask);
+//   - a prefetch past the last round reads the L2-resident table buffer, never HBM;
+//   - XOR trees use v_bitop3_b32 (3-input XOR, new on gfx950);
+//   - a 2-way unrolled loop keeps one round in flight without register copies.
+// Results are not stored per round: on gfx950 stores share vmcnt with loads (a store per
+// round cost 4.3% on the load probe).  The 4 results of a round are shuffled into a
+// collector register (lane 4k + q after k rounds); every 16 rounds the wave applies the
+// trailing-zero fix x^(-8T) and the init constant to all 64 values and stores them with
+// one instruction.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t stag_apply3(const char *lds, const uint32_t (&key)[4], const uint32_t (&sel)[4],
+                                                uint32_t x) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, key[0], sel[0]);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, key[1], sel[1]);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, key[2], sel[2]);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, key[3], sel[3]);
+    return xor3(lds_rd(lds, a0 + OFF), lds_rd(lds, a1 + OFF), lds_rd(lds, a2 + OFF)) ^ lds_rd(lds, a3 + OFF);
+}
+
+// DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by a
+// plain XOR, bit1 skips the combine.  Production instantiations use DIAG = 0.
+template <int ROWS, int FRAME = kBraidFrame, int DIAG = 0, int DEPTH = kBraidDepth>
+__global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, uint32_t *__restrict__ out,
                                                       const uint32_t *__restrict__ gtab, uint32_t cinit) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
 
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwave = blockDim.x >> 6;
     const uint32_t j = lane & (kG - 1);  // braid group (column) within the packet
     const uint32_t q = lane >> 4;        // packet slot within the wave (0..3)
-    const RepKeys K(lane);
+    const StagKeys K(lane);
+    auto inv_plain = [&](uint32_t i, uint32_t v) { return op_apply(lds, kBraidPlainOps + i * kOpBytes, v); };
 
     constexpr uint32_t kFrame = 256u * ROWS;
     const uint64_t rounds = (n + 3) >> 2;
     const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    const uint32_t qoff = q * stride;
+    gu8 *const gbase = (gu8 *)base;
+    gu8 *const dead = (gu8 *)gtab;  // L2-hot, >= 64 KiB
 
-    // Chunk (row i, column j) of a packet lives at frame_start + i*256 + j*16.  Loads are
-    // branch-free and unconditional so the compiler can count them (s_waitcnt vmcnt(N)):
-    // a chunk outside the packet reads a 16-B zero block of the table buffer (no masking
-    // after the load, which would force an immediate wait); a round past the end
-    // re-reads base[0..16).  Addresses are formed from pointers so the loads stay
-    // global_load (flat loads also count on lgkmcnt and stall behind the LDS lookups).
-    const uint8_t *zero16 = reinterpret_cast<const uint8_t *>(gtab + OFF_ZERO);
     struct Round {
         u32x4 w[ROWS];
-        uint32_t trail;
+        uint32_t lead;
     };
+    // Round rr: packets 4rr .. 4rr+3.  rr is wave-uniform.
     auto load_round = [&](uint64_t rr, Round &R) {
         const bool live = rr < rounds;
-        uint64_t p = rr * 4 + q;
-        p = p < n ? p : n - 1;
-        const uint8_t *ps = live ? base + p * stride : base;
-        const uint32_t lead = FRAME ? braid_lead(reinterpret_cast<uintptr_t>(ps), len, kFrame) : kFrame - len;
-        R.trail = kFrame - len - lead;
-        const uint8_t *fs = ps - lead;
+        const uint64_t p0 = rr * 4;
+        gu8 *sb = live ? gbase + p0 * stride : dead;
+        // lanes whose packet is past n re-read packet n-1 (result dropped at the flush)
+        const uint32_t po = (!live || p0 + q < n) ? qoff : uint32_t(n - 1 - p0) * stride;
+        const uint32_t lead =
+            FRAME ? braid_lead(uint32_t(reinterpret_cast<uintptr_t>((const void *)sb)) + po, len, kFrame) : kFrame - len;
+        R.lead = lead;
+        const uint32_t fo = po - lead + j * 16u;  // frame column offset (used by rows >= 1)
 #pragma unroll
         for (int i = 0; i < ROWS; ++i) {
-            const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(lead);
-            const bool ok = rel >= 0 && rel < int32_t(len);
-            const uint8_t *a = ok ? fs + uint32_t(i) * 256u + j * 16u : zero16;
-            R.w[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a));
+            uint32_t o = fo + uint32_t(i) * 256u;
+            if (i == 0 || i == ROWS - 1) {  // may hold frame bytes outside the packet
+                const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(lead);
+                o = (rel >= 0 && rel < int32_t(len)) ? o : po;
+            }
+            R.w[i] = __builtin_nontemporal_load((gu32x4 *)(sb + o));
         }
     };
 
@@ -207,10 +290,10 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     auto flush = [&]() {
         const uint32_t t = colt >> 4;  // x^(-8T), T = 16t
         uint32_t v = col;
-        if (t & 1u) v = op_apply(lds, kRepBytes + 2 * kOpBytes, v);
-        if (t & 2u) v = op_apply(lds, kRepBytes + 3 * kOpBytes, v);
-        if (t & 4u) v = op_apply(lds, kRepBytes + 4 * kOpBytes, v);
-        if (t & 8u) v = op_apply(lds, kRepBytes + 5 * kOpBytes, v);
+        if (t & 1u) v = stag_apply3<128>(lds, K.kB, K.sel, v);  // x^-128
+        if (t & 2u) v = inv_plain(0, v);                        // x^-256
+        if (t & 4u) v = inv_plain(1, v);                        // x^-512
+        if (t & 8u) v = inv_plain(2, v);                        // x^-1024
         const uint64_t rr = rfirst + uint64_t(lane >> 2) * rstep;
         const uint64_t p = rr * 4 + (lane & 3u);
         if ((lane >> 2) < k && rr < rounds && p < n) out[p] = v ^ cinit;
@@ -221,24 +304,45 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
         uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
 #pragma unroll
         for (int i = 0; i < ROWS; ++i) {
-            b0 = rep_word(lds, K, b0 ^ R.w[i].x);
-            b1 = rep_word(lds, K, b1 ^ R.w[i].y);
-            b2 = rep_word(lds, K, b2 ^ R.w[i].z);
-            b3 = rep_word(lds, K, b3 ^ R.w[i].w);
+            u32x4 w = R.w[i];
+            if (i == 0 || i == ROWS - 1) {
+                const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(R.lead);
+                if (!(rel >= 0 && rel < int32_t(len))) w = u32x4{0, 0, 0, 0};
+            }
+            if (DIAG & 1) {
+                b0 = (b0 ^ w.x) + (b0 >> 3);
+                b1 = (b1 ^ w.y) + (b1 >> 3);
+                b2 = (b2 ^ w.z) + (b2 >> 3);
+                b3 = (b3 ^ w.w) + (b3 >> 3);
+                continue;
+            }
+            b0 = stag_apply3<0>(lds, K.kA, K.sel, b0 ^ w.x);
+            b1 = stag_apply3<0>(lds, K.kA, K.sel, b1 ^ w.y);
+            b2 = stag_apply3<0>(lds, K.kA, K.sel, b2 ^ w.z);
+            b3 = stag_apply3<0>(lds, K.kA, K.sel, b3 ^ w.w);
         }
-        // braid b = 4j + k holds R_0(frame_b) * x^(32 b): fold with x^(-32 k), then
-        // across lanes with x^(-128 j).
-        uint32_t v = b0 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b1) ^
-                     op_apply(lds, kRepBytes + 1 * kOpBytes, b2 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b3));
+        // braid b = 4j + k holds R_0(frame_b) * x^(32 b): fold with x^(-32 k) (dense,
+        // conflict-free staggered operators), then across lanes with x^(-128 j).
+        uint32_t v;
+        if (DIAG & 2) {
+            v = xor3(b0, b1, b2) ^ b3;
+        } else {
+        v = xor3(b0, stag_apply3<128>(lds, K.kA, K.sel, b1),
+                 stag_apply3<0>(lds, K.kB, K.sel, b2 ^ stag_apply3<128>(lds, K.kA, K.sel, b3)));
+        {
+            const uint32_t u = __shfl_down(v, 1, kG);
+            if ((j & 1u) == 0) v ^= stag_apply3<128>(lds, K.kB, K.sel, u);  // x^-128
+        }
 #pragma unroll
-        for (uint32_t d = 1, o = 2; d < kG; d <<= 1, ++o) {
+        for (uint32_t d = 2, o = 0; d < kG; d <<= 1, ++o) {
             const uint32_t u = __shfl_down(v, d, kG);
-            if ((j & (2 * d - 1)) == 0) v ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
+            if ((j & (2 * d - 1)) == 0) v ^= inv_plain(o, u);  // x^-256, x^-512, x^-1024
+        }
         }
         // collect: lane 4k + q takes packet slot q's value (held by lane 16q)
         if (k == 0) rfirst = rr;
         const uint32_t src = (lane & 3u) << 4;
-        const uint32_t mv = __shfl(v, src), mt = __shfl(R.trail, src);
+        const uint32_t mv = __shfl(v, src), mt = __shfl(kFrame - len - R.lead, src);
         if ((lane >> 2) == k) {
             col = mv;
             colt = mt;
@@ -247,29 +351,43 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     };
 
     uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
-    // first loads are issued before the LDS table fill so the fill overlaps them
-    Round A, B;
+    // the first loads are issued before the LDS table fill so the fill overlaps them
+    Round A, B, C;
     load_round(r, A);
     if (DEPTH == 2) load_round(r + rstep, B);
-    fill_replicated(lds, gtab + OFF_BRAID);
-    fill_ops(lds, gtab + OFF_INV, 6);
+    fill_stag(lds, 0, 0, gtab + OFF_BRAID);
+    fill_stag(lds, 0, 1, gtab + OFF_INV + 0 * 1024);  // x^-32
+    fill_stag(lds, 1, 0, gtab + OFF_INV + 1 * 1024);  // x^-64
+    fill_stag(lds, 1, 1, gtab + OFF_INV + 2 * 1024);  // x^-128
+    {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kBraidPlainOps);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_INV + 3 * 1024);
+        for (uint32_t i = threadIdx.x; i < 3 * 256; i += blockDim.x) dst[i] = src[i];
+    }
     __syncthreads();
 
-    if (DEPTH == 2) {
+    if (DEPTH == 2) {  // 3 register sets rotate: two rounds in flight while one is hashed
         while (r < rounds) {
+            load_round(r + 2 * rstep, C);
             crc_round(r, A);
-            load_round(r + 2 * rstep, A);
             r += rstep;
             if (r >= rounds) break;
+            load_round(r + 2 * rstep, A);
             crc_round(r, B);
+            r += rstep;
+            if (r >= rounds) break;
             load_round(r + 2 * rstep, B);
+            crc_round(r, C);
             r += rstep;
         }
     } else {
         while (r < rounds) {
-            const Round C = A;
+            load_round(r + rstep, B);
+            crc_round(r, A);
+            r += rstep;
+            if (r >= rounds) break;
             load_round(r + rstep, A);
-            crc_round(r, C);
+            crc_round(r, B);
             r += rstep;
         }
     }
@@ -594,7 +712,8 @@ int launch_check(const char *what) {
 template <int ROWS>
 void launch_braid_rows(dim3 grid, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len, uint64_t n,
                        uint32_t *out, const uint32_t *tabs, uint32_t cinit) {
-    hipLaunchKernelGGL(dev::k_fixed_braid<ROWS>, grid, dim3(1024), 0, st, b, stride, len, n, out, tabs, cinit);
+    hipLaunchKernelGGL(dev::k_fixed_braid<ROWS>, grid, dim3(1024), 0, st, b, uint32_t(stride), len, n, out, tabs,
+                       cinit);
 }
 
 int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
@@ -725,7 +844,9 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t *b = static_cast<const uint8_t *>(d_payloads);
-    const bool fast = len >= 16 && len <= 1536 && len % 16 == 0 && stride % 16 == 0 &&
+    // braided fast path; stride <= 16 KiB keeps every per-lane offset (3 strides + frame)
+    // inside the 74 KB table buffer used as the dead-round prefetch target
+    const bool fast = len >= 16 && len <= 1536 && len % 16 == 0 && stride % 16 == 0 && stride <= 16384 &&
                       reinterpret_cast<uintptr_t>(b) % 16 == 0;
     if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, d_out, st);
     // general kernel, in sub-batches whose byte span stays < 2 GiB

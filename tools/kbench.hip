@@ -201,6 +201,80 @@ __global__ __launch_bounds__(1024) void k_gprobe(const uint8_t *__restrict__ bas
     if (acc == 0x12345678u) out[0] = acc ^ ((LDSF & 1) ? lds_w[lane] : 0u);
 }
 
+// Segment layout probe: 16 lanes per packet, lane j owns the contiguous 96-B segment
+// [frame + 96 j, +96) of a right-aligned 1536-B frame; row i loads 16 B at +16 i.
+template <int DEPTH>
+__global__ __launch_bounds__(1024) void k_seg_probe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint32_t j = lane & 15u, q = lane >> 4;
+    const uint64_t rounds = (n + 3) >> 2;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    uint32_t acc = 0;
+    for (uint64_t r = uint64_t(blockIdx.x) * nwave + wave; r < rounds; r += rstep * DEPTH) {
+        u32x4 w[DEPTH][6];
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd) {
+            uint64_t p = (r + dd * rstep) * 4 + q;
+            p = p < n ? p : n - 1;
+            const uint8_t *fs = base + p * 1456 + 1456 - 1536;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const uint32_t o = j * 96u + i * 16u;
+                w[dd][i] = o >= 80u ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + o)) : u32x4{0, 0, 0, 0};
+            }
+        }
+#pragma unroll
+        for (int dd = 0; dd < DEPTH; ++dd)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) acc ^= w[dd][i].x ^ w[dd][i].y ^ w[dd][i].z ^ w[dd][i].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Stage-through-LDS probes: a wave's 4 packets (5824 contiguous bytes) are read as six
+// contiguous 1 KiB pieces, written to a per-wave 6 KiB LDS slot, and read back in the braid
+// layout (lane (q, j), row i <- packet q chunk 16 i + j, right-aligned 1536-B frame).
+// DMA = 0: global_load_dwordx4 + ds_write_b128; DMA = 1: global_load_lds_dwordx4.
+template <int DMA>
+__global__ __launch_bounds__(1024) void k_stage_probe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[16 * 6144];
+    const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwave = blockDim.x >> 6;
+    const uint32_t j = lane & 15u, q = lane >> 4;
+    uint8_t *slot = stage + wave * 6144;
+    const uint64_t rounds = (n + 3) >> 2;
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    const uint64_t total = n * 1456;
+    gu8 *gb = (gu8 *)base;
+    uint32_t acc = 0;
+    for (uint64_t r = uint64_t(blockIdx.x) * nwave + wave; r < rounds; r += rstep) {
+        const uint64_t r0 = r * 4 * 1456;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            uint64_t o = r0 + uint64_t(i) * 1024 + lane * 16;
+            o = o + 16 <= total ? o : 0;
+            if (DMA) {
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(gb + o),
+                                                 (__attribute__((address_space(3))) void *)(slot + i * 1024), 16, 0, 0);
+            } else {
+                const u32x4 v = __builtin_nontemporal_load((gu32x4 *)(gb + o));
+                *reinterpret_cast<u32x4 *>(slot + i * 1024 + lane * 16) = v;
+            }
+        }
+        if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int32_t o = int32_t(q * 1456u) - 80 + i * 256 + int32_t(j * 16u);
+            if (o >= int32_t(q * 1456u)) {
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(slot + o);
+                acc ^= v.x ^ v.y ^ v.z ^ v.w;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 int main(int argc, char **argv) {
@@ -224,11 +298,14 @@ int main(int argc, char **argv) {
     vs.push_back({"read_probe_g256x1024", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(1024), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
-    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f0_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f1_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"new_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"new_nocomb_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"new_nolut", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"new_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"new_nolut_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
     vs.push_back({"braid_old_rightaligned", [&] { hipLaunchKernelGGL((k_braid_diag<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
     vs.push_back({"braid_nolut", [&] { hipLaunchKernelGGL((k_braid_diag<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
     vs.push_back({"braid_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
@@ -245,6 +322,10 @@ int main(int argc, char **argv) {
     GP(8, 12, 0, 1, 256, 1024); GP(8, 12, 1, 1, 256, 1024); GP(8, 12, 1, 2, 256, 1024);
     GP(32, 3, 0, 2, 256, 1024); GP(32, 3, 1, 2, 256, 1024); GP(32, 3, 1, 4, 256, 1024);
     GP(16, 6, 1, 2, 512, 512); GP(8, 12, 1, 1, 512, 512);
+    vs.push_back({"stage_probe_reg", [&] { hipLaunchKernelGGL((k_stage_probe<0>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
+    vs.push_back({"stage_probe_dma", [&] { hipLaunchKernelGGL((k_stage_probe<1>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
+    vs.push_back({"seg_probe_d1", [&] { hipLaunchKernelGGL((k_seg_probe<1>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
+    vs.push_back({"seg_probe_d2", [&] { hipLaunchKernelGGL((k_seg_probe<2>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
 #define GPL(G, R, AL, D, F) vs.push_back({"gprobe_G" #G "_R" #R "_al" #AL "_d" #D "_ldsf" #F, [&] { hipLaunchKernelGGL((k_gprobe<G, R, AL, D, F>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out, s.tabs); }, {}})
     GPL(16, 6, 1, 1, 1); GPL(16, 6, 1, 1, 2); GPL(16, 6, 1, 1, 3); GPL(16, 6, 0, 1, 3);
     vs.push_back({"pieces_fixed", [&] {  // general kernel, fixed provider
@@ -265,7 +346,7 @@ int main(int argc, char **argv) {
         }
     // sustained: 200 back-to-back launches per selected variant (DVFS steady state)
     if (getenv("KB_SUSTAIN")) {
-        const int NS = 200;
+        const int NS = getenv("KB_NS") ? atoi(getenv("KB_NS")) : 200;
         std::vector<hipEvent_t> ev(NS + 1);
         for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
         for (auto &v : vs) {
