@@ -49,15 +49,15 @@ constexpr int kG = 16;                       // lanes per packet in the braided 
 constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
 constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
 constexpr int kPieceS = 64;                  // piece bytes in the general kernel
-constexpr uint32_t kMaxVarLen = 4096;        // 64 pieces x 64 B: one packet per wave max
+constexpr uint32_t kMaxVarLen = 4096;
+constexpr uint64_t kSubBatch = 1ull << 28;      // packets per general-kernel launch (32-bit store offsets)        // 64 pieces x 64 B: one packet per wave max
 
 constexpr uint32_t OFF_BRAID = 0;            // 4x256 braid word tables (advance 256 B)
 constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-256, x^-512, x^-1024
 constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
 constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
-constexpr uint32_t OFF_CINIT = OFF_FWD + 6 * 1024;  // init_const(L), L = 0..4096
-constexpr uint32_t OFF_ZERO = (OFF_CINIT + kMaxVarLen + 1 + 3) & ~3u;  // 16 zero bytes (braid masking)
-constexpr uint32_t TAB_WORDS = OFF_ZERO + 4;
+constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
+constexpr uint32_t TAB_WORDS = OFF_HINIT + 68;
 
 // LDS images.  Replicated word tables: byte address
 //   t_hi*65536 + e*256 + t_lo*128 + (lane&31)*4   for table t = 2*t_hi + t_lo,
@@ -73,6 +73,7 @@ constexpr uint32_t kBraidLdsWords = (kBraidPlainOps + 3 * kOpBytes) / 4;  // 143
 namespace dev {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // Explicit global (address space 1) pointers for the streaming loads: a select between
 // two generic pointers defeats address-space inference and degrades to flat_load, which
 // also counts on lgkmcnt and serialises with the LDS lookups.
@@ -397,27 +398,35 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
 // ------------------------------------------------------------------------------------
 // 2. pieces kernel (general shapes)
 // ------------------------------------------------------------------------------------
+// Epilogues store through buffer resources: lanes without a result use an out-of-range
+// offset, so the store is one unconditional instruction (no exec branch, so the
+// compiler's vmcnt accounting keeps the round's prefetches in flight).  n < 2^29 (the
+// host splits larger batches).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes);
+// Raw metadata words of one packet as loaded by a provider (see the providers below).
+struct MetaRaw {
+    uint64_t a;
+    uint32_t b, c, d;
+};
 struct CrcEpi {
-    uint32_t *__restrict__ out;
-    __device__ __forceinline__ void put(const uint8_t *, uint64_t p, uint64_t, uint32_t crc, bool) const {
-        out[p] = crc;
+    uint32_t *out;
+    uint32_t n;
+    __device__ __forceinline__ void put(uint64_t p, uint32_t crc, bool, uint32_t, bool on) const {
+        __builtin_amdgcn_raw_buffer_store_b32(crc, make_rsrc(out, 4 * n), on ? int(4 * p) : int(0x80000000u), 0, 0);
     }
 };
-struct VerifyEpi {  // Receiver.cpp:203-206: (int)ntohl(hdr.checksum) == (int)crc32(payload)
-    uint8_t *__restrict__ ok_out;
-    uint32_t *__restrict__ crc_out;  // may be null
-    __device__ __forceinline__ void put(const uint8_t *base, uint64_t p, uint64_t off, uint32_t crc,
-                                        bool valid) const {
-        bool ok = false;
-        if (valid) {
-            const uint8_t *h = base + off - 4;  // header.checksum, big-endian on the wire
-            const uint32_t want = (uint32_t(h[0]) << 24) | (uint32_t(h[1]) << 16) | (uint32_t(h[2]) << 8) | h[3];
-            ok = want == crc;
-        } else {
-            crc = 0;
-        }
-        ok_out[p] = ok ? 1 : 0;
-        if (crc_out) crc_out[p] = crc;
+// Receiver.cpp:203-206: (int)ntohl(hdr.checksum) == (int)crc32(payload).  aux carries the
+// header checksum (host order) from the provider.
+struct VerifyEpi {
+    uint8_t *ok;
+    uint32_t *crc;  // may be null
+    uint32_t n;
+    __device__ __forceinline__ void put(uint64_t p, uint32_t c, bool valid, uint32_t want, bool on) const {
+        const bool good = valid && want == c;
+        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(good ? 1 : 0), make_rsrc(ok, n), on ? int(p) : int(0x80000000u),
+                                             0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(valid ? c : 0u, make_rsrc(crc, crc ? 4 * n : 0u),
+                                              on ? int(4 * p) : int(0x80000000u), 0, 0);
     }
 };
 
@@ -430,87 +439,186 @@ __device__ __forceinline__ u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
 
+// LDS of k_pieces: region 0 holds two staggered table sets (set 0 = slice-by-4, set 1 =
+// the x^(8*64) scan operator), then the scan operators x^(8*64*d), d = 2..32, as plain
+// 4 KiB tables, the 65-word head-init table, and one staging slot per wave.  A slot
+// holds a span of 16-B chunks with 16 B of padding after every 256 B (chunk c at
+// 16*(c + c/16)): the windows of consecutive pieces are 64 B apart, and the padding
+// spreads their 16-B reads over all bank groups instead of four.
+constexpr uint32_t kPcOps = 65536;
+constexpr uint32_t kPcHinit = kPcOps + 5 * kOpBytes;
+constexpr uint32_t kPcStage = kPcHinit + 272;
+constexpr uint32_t kPcChunks = 272;  // span chunks a slot holds: 64 pieces + gaps + head slack
+constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read one chunk past
+constexpr uint32_t kPcLdsWords = (kPcStage + 16 * kPcSlot) / 4;  // 160,528 B
+static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
+static_assert(kPcLdsWords * 4 <= 163840, "LDS");
+
+__device__ __forceinline__ uint32_t stage_addr(uint32_t chunk) { return 16u * (chunk + (chunk >> 4)); }
+
+// Lane-contiguous load of kPcChunks 16-B chunks starting at view offset b16 (16-aligned,
+// may be negative near the buffer start): 4 full wave instructions + 16 lanes of a
+// fifth.  Offsets outside the buffer read 0 without touching memory.
+__device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16, uint32_t lane, u32x4 (&x)[5]) {
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i) {
+        const uint32_t c = 64u * i + lane;
+        x[i] = buf_ld16(rs, c < kPcChunks ? uint32_t(b16) + 16u * c : 0x80000000u);
+    }
+}
+
+// The wave's packets form one stream of 64-B pieces (each packet cut into pieces counted
+// back from its end, the head piece possibly shorter).  A round takes the next pieces,
+// one per lane, up to 64 and up to the first piece whose window falls outside the span
+// one LDS slot holds (kPcChunks chunks from the round's first window): packed and
+// strided batches always fill all 64 lanes, scattered offsets make shorter rounds.  A
+// packet may straddle rounds: its CRC register after its last piece in round r seeds the
+// chain of its next piece in round r+1.  Per round a wave
+//   1. scans the piece counts of the next 64 packets (metadata prefetched during the
+//      previous round) and assigns lane -> (packet, piece);
+//   2. stages the span into its LDS slot: it was loaded during the previous round (it
+//      starts at most 64 B before that round's last window ends: speculative, exact for
+//      packed and strided batches); a miss loads it now.  All global loads are
+//      lane-contiguous 16-B chunks, 1 KiB per wave instruction;
+//   3. reads each lane's 64-B window from the slot and issues the next round's metadata
+//      and span loads;
+//   4. runs the slice-by-4 chain over the window (bytes before the packet masked to
+//      zero; the head piece adds shift(~0, head length), the CRC's initial value), then a
+//      segmented scan with x^(8*64*d) combines each packet's pieces and the lane holding
+//      a packet's last piece emits crc = W ^ ~0.
+// Loads and stores are branch-free (out-of-range buffer offsets for idle lanes), so the
+// prefetches stay in flight across the round.
 template <class Prov, class Epi>
 __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
                                                  uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
                                                  uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
-    fill_replicated(lds, gtab + OFF_S4);
-    fill_ops(lds, gtab + OFF_FWD, 6);
+    fill_stag(lds, 0, 0, gtab + OFF_S4);
+    fill_stag(lds, 0, 1, gtab + OFF_FWD);
+    {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kPcOps);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024);
+        for (uint32_t i = threadIdx.x; i < 5 * 256; i += blockDim.x) dst[i] = src[i];
+        if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = gtab[OFF_HINIT + threadIdx.x];
+    }
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t gw = uint64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t gw = uint64_t(blockIdx.x) * (blockDim.x >> 6) + wave;
     const uint64_t tw = uint64_t(gridDim.x) * (blockDim.x >> 6);
     const uint64_t lo = n * gw / tw, hi = n * (gw + 1) / tw;
-    const RepKeys K(lane);
+    const StagKeys K(lane);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
+    char *slot = lds + kPcStage + wave * kPcSlot;
+    constexpr int32_t kSpanBytes = int32_t(16 * kPcChunks);
+    constexpr int32_t kNoSpan = 0x7FFFF000;  // out of range: loads return 0, no traffic
 
+    // lane i describes packet q0 + i (clamped to hi - 1: branch-free)
+    MetaRaw raw{};
+    auto meta = [&](uint64_t q0) {
+        const uint64_t pi = q0 + lane;
+        prov.load(pi < hi ? pi : hi - 1, raw, rs);
+    };
+    if (lo < hi) meta(lo);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loop entry then matches its back edge
+
+    uint32_t skip = 0, carry = 0;  // pieces of packet p0 done in earlier rounds, their register
+    int32_t spec = kNoSpan;        // view offset of the prefetched span
+    u32x4 x[5];
     for (uint64_t p0 = lo; p0 < hi;) {
-        // --- this round's packets: lane i describes packet p0 + i ----------------------
-        const uint64_t pi = p0 + lane;
-        const bool have = pi < hi;
-        uint64_t off = 0;
-        uint32_t len = 0;
-        bool valid = false;
-        if (have) prov.get(pi, off, len, valid);
+        uint64_t off;
+        uint32_t len, aux = 0;
+        bool valid;
+        prov.decode(raw, off, len, valid, aux);
+        const bool have = p0 + lane < hi;
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
             len = 0;
             valid = false;
         }
-        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 65u;
-        uint32_t incl = k;
+        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 64u;
+        const uint32_t kr = k - (lane == 0 ? skip : 0u);  // pieces still to do
+        uint32_t incl = kr;
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
             const uint32_t u = __shfl_up(incl, d);
             if (lane >= d) incl += u;
         }
-        const uint64_t fitmask = __ballot(have && incl <= 64u);
-        const uint32_t m = __popcll(fitmask);  // >= 1: a packet has <= 64 pieces
-        const uint32_t total = __shfl(incl, m - 1);
+        const uint32_t navail = __popcll(__ballot(have));  // packets of the wave left in view
 
-        // --- lane -> (packet, piece): pk = #packets whose pieces all precede this lane -
+        // --- lane -> (packet, piece): pk = #packets whose pieces all precede this lane ---
         uint32_t pk = 0;
 #pragma unroll
         for (uint32_t s = 32; s >= 1; s >>= 1) {
             const uint32_t probe = pk + s - 1;
             const uint32_t v = __shfl(incl, probe & 63u);
-            if (probe < m && v <= lane) pk += s;
+            if (probe < navail && v <= lane) pk += s;
         }
-        const bool active = lane < total;
-        pk = active ? pk : 0;
+        const bool mapped = pk < navail;
+        pk = mapped ? pk : 0;
         const uint32_t pinc = __shfl(incl, pk);
+        const uint32_t pkr = __shfl(kr, pk);
         const uint32_t pkk = __shfl(k, pk);
         const uint32_t plen = __shfl(len, pk);
-        const uint32_t poff_lo = __shfl(uint32_t(off), pk);
-        const uint32_t poff_hi = __shfl(uint32_t(off >> 32), pk);
+        const uint32_t poff = __shfl(uint32_t(off), pk);  // < 2^31: the view is < 2 GiB
         const bool pvalid = __shfl(valid ? 1u : 0u, pk) != 0;
-        const uint64_t poff = (uint64_t(poff_hi) << 32) | poff_lo;
-        const uint32_t piece = lane - (pinc - pkk);  // 0 = head piece
+        const uint32_t paux = __shfl(aux, pk);
+        const uint32_t lp = lane - (pinc - pkr);         // piece index within this round
+        const uint32_t gp = lp + (pk == 0 ? skip : 0u);  // piece index within the packet
 
         // --- piece window: the 64 bytes ending at this piece's end ----------------------
-        // Pieces are counted back from the packet end, so every window is exactly 64 B;
-        // the head window also covers up to 64 bytes before the packet, which are
-        // masked to zero (free: R_0(0^k || M) = R_0(M)).
-        const int64_t we = int64_t(poff + plen) - int64_t(pkk - 1 - piece) * kPieceS;
-        const int64_t ws = we - kPieceS;
-        const int64_t vf64 = int64_t(poff) - ws;  // bytes of the window before the packet
-        const int32_t vf = active ? int32_t(vf64 > 64 ? 64 : vf64) : 64;
-        const uint32_t a = uint32_t(uint64_t(ws) & 15u);
-        const uint32_t blk = uint32_t(uint64_t(ws - int64_t(a)));  // may wrap: OOB -> 0
+        const int32_t we = int32_t(poff + plen) - int32_t(pkk - 1 - gp) * kPieceS;
+        const int32_t ws = we - kPieceS;
+        // the round: lanes up to the first one whose window leaves [lo16, lo16 + span)
+        const int32_t lo16 = __builtin_amdgcn_readfirstlane(__shfl(ws, 0)) & ~15;
+        const bool out = !mapped || ws < lo16 || we - lo16 > kSpanBytes;
+        const uint64_t outm = __ballot(out);
+        const uint32_t total = outm ? uint32_t(__builtin_ctzll(outm)) : 64u;  // >= 1: lane 0 fits
+        const bool active = lane < total;
+        const int32_t vf0 = int32_t(poff) - ws;  // bytes of the window before the packet
+        const int32_t vf = active ? (vf0 > 64 ? 64 : vf0) : 64;
+        const uint32_t a = uint32_t(ws) & 15u;
 
-        uint32_t d[20];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            u32x4 x = {0, 0, 0, 0};
-            if (active && vf < 16 * (u + 1)) x = buf_ld16(rs, blk + 16u * u);
-            d[4 * u + 0] = x.x;
-            d[4 * u + 1] = x.y;
-            d[4 * u + 2] = x.z;
-            d[4 * u + 3] = x.w;
+        // --- stage the span ---------------------------------------------------------------
+        const bool hit = __ballot(active && (ws < spec || we - spec > kSpanBytes)) == 0;
+        int32_t sbase = spec;
+        if (!hit) {
+            load_span(rs, lo16, lane, x);
+            sbase = lo16;
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the miss pays its latency here
         }
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) *reinterpret_cast<u32x4 *>(slot + stage_addr(64u * i + lane)) = x[i];
+        if (lane < kPcChunks - 256u) *reinterpret_cast<u32x4 *>(slot + stage_addr(256u + lane)) = x[4];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t d[20];
+        {
+            const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 5; ++u) {
+                const u32x4 y = *reinterpret_cast<const u32x4 *>(slot + stage_addr(blk + u));
+                d[4 * u + 0] = y.x;
+                d[4 * u + 1] = y.y;
+                d[4 * u + 2] = y.z;
+                d[4 * u + 3] = y.w;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+
+        // --- round bookkeeping and the next round's prefetch ------------------------------
+        const uint32_t tl = total - 1;
+        const uint32_t last_pk = __builtin_amdgcn_readfirstlane(__shfl(pk, tl));
+        const uint32_t last_gp = __builtin_amdgcn_readfirstlane(__shfl(gp, tl));
+        const uint32_t last_k = __builtin_amdgcn_readfirstlane(__shfl(pkk, tl));
+        const int32_t last_we = __builtin_amdgcn_readfirstlane(__shfl(we, tl));
+        const bool partial = last_gp + 1 < last_k;
+        const uint64_t p0n = p0 + last_pk + (partial ? 0u : 1u);
+        meta(p0n);  // first: the next round waits for these, not for the span
+        spec = p0n < hi ? ((last_we - kPieceS) & ~15) : kNoSpan;
+        load_span(rs, spec, lane, x);
+
         // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
         const uint32_t m2 = 0u - ((a >> 3) & 1u), m1 = 0u - ((a >> 2) & 1u), sb = a & 3u;
         uint32_t e[18];
@@ -519,29 +627,34 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 #pragma unroll
         for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
 
-        uint32_t c = 0;
+        uint32_t c = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
             // keep bytes at window offset >= vf
             const int32_t sh = vf - 4 * i;
             const uint32_t keep = sh <= 0 ? 0xFFFFFFFFu : (sh >= 4 ? 0u : (0xFFFFFFFFu << (8 * sh)));
-            wd &= keep;
-            c = rep_word(lds, K, c ^ wd);
+            c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (wd & keep));
         }
+        // head piece: R_~0(head) = R_0(0^vf || head) ^ shift(~0, 64 - vf)
+        const uint32_t hw = lds_rd(lds, kPcHinit + 4u * uint32_t(kPieceS - (vf < 0 ? 0 : vf)));
+        c ^= gp == 0u ? hw : 0u;
 
         // --- segmented inclusive scan: W_i <- W_{i-d} * x^(8*64*d) ^ W_i ---------------
         uint32_t W = c;
+        {
+            const uint32_t u = __shfl_up(W, 1);
+            if (lp >= 1u && lane >= 1u) W ^= stag_apply<128>(lds, K.kA, K.sel, u);
+        }
 #pragma unroll
-        for (uint32_t dd = 1, o = 0; dd < 64; dd <<= 1, ++o) {
+        for (uint32_t dd = 2, o = 0; dd < 64; dd <<= 1, ++o) {
             const uint32_t u = __shfl_up(W, dd);
-            if (piece >= dd && lane >= dd) W ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
+            if (lp >= dd && lane >= dd) W ^= op_apply(lds, kPcOps + o * kOpBytes, u);
         }
-        if (active && piece == pkk - 1) {
-            const uint32_t crc = W ^ gtab[OFF_CINIT + plen];
-            epi.put(base, p0 + pk, poff, crc, pvalid);
-        }
-        p0 += m;
+        epi.put(p0 + pk, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
+        carry = partial ? uint32_t(__shfl(W, tl)) : 0u;
+        skip = partial ? last_gp + 1 : 0u;
+        p0 = p0n;
     }
 }
 
@@ -658,11 +771,7 @@ std::vector<uint32_t> host_tables() {
         const uint64_t nb = uint64_t(kPieceS) << o;
         make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
     }
-    uint32_t ff = 0xFFFFFFFFu;  // init_const(L) incrementally
-    for (uint32_t L = 0; L <= kMaxVarLen; ++L) {
-        t[OFF_CINIT + L] = ff ^ 0xFFFFFFFFu;
-        ff = shift_bytes(ff, 1);
-    }
+    for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
     return t;
 }
 
@@ -759,11 +868,15 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
 // Offsets handed to k_pieces must be relative to the 16-B aligned view.  The providers
 // below add `lead` back.
 namespace dev {
+// Providers split metadata access in two: load() only issues loads (its results are
+// consumed a round later, so no arithmetic may touch them there) and decode() turns the
+// raw words into (offset in the view, length, valid, aux) when the round uses them.
 struct FixedProvL {
     uint64_t stride, lead;
     uint32_t len;
-    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
-        off = lead + p * stride;
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &) const {
+        off = lead + r.a * stride;
         l = len;
         ok = true;
     }
@@ -772,20 +885,39 @@ struct ArrayProvL {
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
-    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
-        off = lead + offs[p];
-        l = lens[p];
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
+        r.a = reinterpret_cast<const uint32_t *>(offs)[2 * p];  // low dword: the view is < 2 GiB
+        r.b = lens[p];
+    }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &) const {
+        off = lead + r.a;
+        l = r.b;
         ok = true;
     }
 };
+// Datagram p = view[lead + p*stride, +recv_len[p]): header (16 B) + payload.  aux =
+// ntohl(header.checksum): the two dwords covering header bytes 12..15 ride with the
+// metadata prefetch (through the view's buffer resource: the second dword may lie past
+// the last datagram, reads there return 0 and are never selected) and are
+// funnel-shifted at decode.
 struct DgramProvL {
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
-    __device__ __forceinline__ void get(uint64_t p, uint64_t &off, uint32_t &l, bool &ok) const {
-        const uint32_t r = rl[p];
-        off = lead + p * stride + 16;
-        ok = r >= 16 && r <= stride;
-        l = ok ? r - 16 : 0;
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
+        const uint32_t h = uint32_t(lead + p * stride + 12) & ~3u;  // the view is < 2 GiB
+        r.a = p;
+        r.b = rl[p];
+        const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(h), 0, 0));
+        r.c = w.x;
+        r.d = w.y;
+    }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok,
+                                           uint32_t &want) const {
+        const uint64_t d = lead + r.a * stride;
+        want = bswap32(__builtin_amdgcn_alignbyte(r.d, r.c, uint32_t(d + 12) & 3u));
+        off = d + 16;
+        ok = r.b >= 16 && r.b <= stride;
+        l = ok ? r.b - 16 : 0;
     }
 };
 }  // namespace dev
@@ -850,13 +982,14 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
                       reinterpret_cast<uintptr_t>(b) % 16 == 0;
     if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, d_out, st);
     // general kernel, in sub-batches whose byte span stays < 2 GiB
-    const uint64_t per = stride ? std::max<uint64_t>(1, ((1ull << 30) - 4096) / stride) : n;
+    const uint64_t per = std::min<uint64_t>(kSubBatch, stride ? std::max<uint64_t>(1, ((1ull << 30) - 4096) / stride) : n);
     for (uint64_t p = 0; p < n; p += per) {
         const uint64_t cnt = std::min<uint64_t>(per, n - p);
         const uint8_t *sb = b + p * stride;
         const uint64_t lead = reinterpret_cast<uintptr_t>(sb) & 15u;
         const uint64_t span = (cnt - 1) * stride + len;
-        rc = launch_pieces(*s, sb, span, dev::FixedProvL{stride, lead, uint32_t(len)}, cnt, dev::CrcEpi{d_out + p}, st);
+        rc = launch_pieces(*s, sb, span, dev::FixedProvL{stride, lead, uint32_t(len)}, cnt,
+                           dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
         if (rc) return rc;
     }
     return WTP_OK;
@@ -871,8 +1004,13 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     if (rc) return rc;
     const uint8_t *b = static_cast<const uint8_t *>(d_base);
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
-    return launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets, d_lengths, lead}, n, dev::CrcEpi{d_out},
-                         static_cast<hipStream_t>(stream));
+    for (uint64_t p = 0; p < n; p += kSubBatch) {
+        const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
+        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
+                           dev::CrcEpi{d_out + p, uint32_t(cnt)}, static_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
+    return WTP_OK;
 }
 
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len, size_t n,
@@ -884,10 +1022,17 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     int rc = current(s);
     if (rc) return rc;
     const uint8_t *b = static_cast<const uint8_t *>(d_dgrams);
-    const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
-    const uint64_t span = uint64_t(n) * stride;
-    return launch_pieces(*s, b, span, dev::DgramProvL{stride, lead, d_recv_len}, n, dev::VerifyEpi{d_ok, d_crc_out},
-                         static_cast<hipStream_t>(stream));
+    const uint64_t per = std::min<uint64_t>(kSubBatch, std::max<uint64_t>(1, (1ull << 30) / stride));
+    for (uint64_t p = 0; p < n; p += per) {
+        const uint64_t cnt = std::min<uint64_t>(per, n - p);
+        const uint8_t *sb = b + p * stride;
+        const uint64_t lead = reinterpret_cast<uintptr_t>(sb) & 15u;
+        rc = launch_pieces(*s, sb, cnt * stride, dev::DgramProvL{stride, lead, d_recv_len + p}, cnt,
+                           dev::VerifyEpi{d_ok + p, d_crc_out ? d_crc_out + p : nullptr, uint32_t(cnt)},
+                           static_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
+    return WTP_OK;
 }
 
 int wtp_synth_fill(void *d_out, uint64_t start_byte, size_t nbytes, uint64_t seed, void *stream) {

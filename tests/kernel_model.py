@@ -123,3 +123,115 @@ def pieces_crc(T: Tables, buf: bytes, off: int, L: int) -> int:
         W = nW
         d *= 2
     return W[K - 1] ^ T.init_const(L)
+
+
+# ---- k_pieces round structure (staging + lane assignment) --------------------------
+PC_CHUNKS = 272
+PC_SLOT = 4640
+SPAN = 16 * PC_CHUNKS
+
+
+def stage_addr(chunk: int) -> int:
+    return 16 * (chunk + (chunk >> 4))
+
+
+def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
+    """One wave of k_pieces over packets (offs[i], lens[i]) of `buf` (the 16-B aligned
+    view; reads outside it return 0 as the buffer resource does).  Mirrors the round
+    loop of csrc/crc32_kernels.hip: the piece stream with carry/skip across rounds, the
+    round cut at the first window outside the slot span, the speculative span prefetch
+    (hit/miss), lane-contiguous staging into a padded slot that still holds older bytes,
+    5 x 16-B window reads, masking, the head-init table, chain and segmented scan.
+    Returns (crcs, rounds, hits)."""
+    rng = rng or np.random.default_rng(0)
+    buf = bytes(buf) + bytes(-len(buf) % 16)  # the host rounds the resource up to 16 B
+    nb = len(buf)
+    hinit = [O.shift(0xFFFFFFFF, h) for h in range(S + 1)]
+
+    def rd16(o):  # raw buffer load of 16 B at u32 offset o
+        o &= 0xFFFFFFFF
+        return bytes(16) if o + 16 > nb else buf[o:o + 16]
+
+    def load_span(b16):
+        return [rd16(b16 + 16 * c) for c in range(PC_CHUNKS)]
+
+    slot = bytearray(rng.integers(0, 256, PC_SLOT, dtype=np.uint8).tobytes())
+    n = len(lens)
+    out = [None] * n
+    p0 = skip = carry = 0
+    spec, x = None, None
+    rounds = hits = 0
+    while p0 < n:
+        navail = min(64, n - p0)
+        ks = [1 if lens[p0 + i] == 0 else (int(lens[p0 + i]) + S - 1) // S for i in range(navail)]
+        kr = list(ks)
+        kr[0] -= skip
+        incl = list(np.cumsum(kr))
+        lanes = []
+        for lane in range(64):
+            pk = sum(1 for j in range(navail) if incl[j] <= lane)
+            if pk >= navail:
+                lanes.append(None)
+                continue
+            lp = lane - (incl[pk] - kr[pk])
+            gp = lp + (skip if pk == 0 else 0)
+            off, L, K = int(offs[p0 + pk]), int(lens[p0 + pk]), ks[pk]
+            we = off + L - (K - 1 - gp) * S
+            lanes.append((pk, lp, gp, off, L, K, we - S, we))
+        lo16 = lanes[0][6] & ~15
+        total = 64
+        for lane, v in enumerate(lanes):
+            if v is None or v[6] < lo16 or v[7] - lo16 > SPAN:
+                total = lane
+                break
+        assert total >= 1
+        act = lanes[:total]
+        hit = spec is not None and all(ws >= spec and we - spec <= SPAN for *_, ws, we in act)
+        if hit:
+            hits += 1
+            sbase = spec
+        else:
+            x, sbase = load_span(lo16), lo16
+        for c in range(PC_CHUNKS):
+            a = stage_addr(c)
+            assert a + 16 <= PC_SLOT
+            slot[a:a + 16] = x[c]
+        # next round (prefetch)
+        pk_l, lp_l, gp_l, _, _, K_l, _, we_l = act[-1]
+        partial = gp_l + 1 < K_l
+        p0n = p0 + pk_l + (0 if partial else 1)
+        spec = (we_l - S) & ~15 if p0n < n else None
+        x = load_span(spec) if spec is not None else None
+        vals = []
+        for lane, (pk, lp, gp, off, L, K, ws, we) in enumerate(act):
+            a = ws & 15
+            blk = (ws - sbase) >> 4
+            assert blk >= 0 and stage_addr(blk + 4) + 16 <= PC_SLOT
+            raw = b"".join(bytes(slot[stage_addr(blk + u):stage_addr(blk + u) + 16]) for u in range(5))
+            window = bytearray(raw[a:a + S])
+            vf = min(off - ws, 64)
+            for t in range(max(vf, 0)):
+                window[t] = 0
+            c = carry if lane == 0 else 0
+            for i in range(16):
+                c = _apply(T.s4, c ^ int.from_bytes(window[4 * i:4 * i + 4], "little"))
+            if gp == 0:
+                c ^= hinit[S - max(vf, 0)]
+            vals.append(c)
+        W = list(vals)
+        d = 1
+        while d < 64:
+            nW = list(W)
+            for i in range(total):
+                if act[i][1] >= d:
+                    nW[i] = _apply(T.fwd[d], W[i - d]) ^ W[i]
+            W = nW
+            d *= 2
+        for i, (pk, lp, gp, off, L, K, ws, we) in enumerate(act):
+            if gp == K - 1:
+                out[p0 + pk] = W[i] ^ 0xFFFFFFFF
+        carry = W[total - 1] if partial else 0
+        skip = gp_l + 1 if partial else 0
+        p0 = p0n
+        rounds += 1
+    return out, rounds, hits

@@ -25,3 +25,38 @@ def test_pieces_model(T, L):
     for off in (0, 1, 5, 13, 100):
         if off + L <= len(buf):
             assert pieces_crc(T, buf, off, L) == O.crc32(buf[off:off + L]), (L, off)
+
+
+@pytest.mark.parametrize("case", ["packed_zipf", "strided_odd", "scattered", "dgram", "edge_start", "big"])
+def test_pieces_rounds_model(T, case):
+    """Round-level model of k_pieces (piece stream, carry across rounds, speculative
+    span prefetch, padded LDS staging) against the oracle."""
+    from kernel_model import pieces_rounds
+    rng = np.random.default_rng(7)
+    if case == "packed_zipf":
+        lens = O.zipf_lengths(300, s=1.0)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + 5
+    elif case == "strided_odd":
+        lens = np.full(40, 1457 - 8, dtype=np.int64)
+        offs = 3 + 1457 * np.arange(40)
+    elif case == "scattered":
+        lens = rng.integers(0, 200, 200)
+        offs = rng.permutation(200) * 300 + rng.integers(0, 16, 200)
+    elif case == "dgram":
+        lens = np.array([1456, 0, 700, 1456, 33, 1456, 1456] * 8)
+        offs = 1472 * np.arange(len(lens)) + 16
+    elif case == "big":  # 4096-B packets: 64 pieces each, every round one whole packet
+        lens = np.array([4096, 4095, 4033, 4096, 1, 4096])
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + 9
+    else:  # packets at the very start and end of the buffer, lengths 0/1/64/4096
+        lens = np.array([1, 64, 0, 4096, 63, 65, 2, 4096, 1456])
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    offs = [int(o) for o in offs]
+    lens = [int(v) for v in lens]
+    nbytes = max(o + v for o, v in zip(offs, lens)) + 7
+    buf = O.synth_fill_np(nbytes, start_byte=11).tobytes()
+    got, rounds, hits = pieces_rounds(T, buf, offs, lens, rng)
+    want = [O.crc32(buf[o:o + v]) for o, v in zip(offs, lens)]
+    assert got == want
+    if case in ("packed_zipf", "strided_odd"):
+        assert hits == rounds - 1  # every round after the first is prefetched

@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests -> bench -> rocprofv3 kernel-trace stats.
 # Every GPU step has its own time limit; a crash-type exit (fault, abort, segfault,
 # time limit) ends the script without starting further GPU work.
-#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra
+#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg smoke
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -41,6 +41,7 @@ for s in $STEPS; do
              -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
            cd "$ROOT" ;;
     extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
+    cfg)   run cfg 600 python tools/bench_configs.py --only "${CFG_ONLY:-c5,verify}" --out "$OUT/configs.json" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

@@ -329,7 +329,7 @@ int main(int argc, char **argv) {
 #define GPL(G, R, AL, D, F) vs.push_back({"gprobe_G" #G "_R" #R "_al" #AL "_d" #D "_ldsf" #F, [&] { hipLaunchKernelGGL((k_gprobe<G, R, AL, D, F>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out, s.tabs); }, {}})
     GPL(16, 6, 1, 1, 1); GPL(16, 6, 1, 1, 2); GPL(16, 6, 1, 1, 3); GPL(16, 6, 0, 1, 3);
     vs.push_back({"pieces_fixed", [&] {  // general kernel, fixed provider
-        launch_pieces(s, buf, bytes, dev::FixedProvL{1456, 0, 1456u}, n, dev::CrcEpi{out}, nullptr); }, {}});
+        launch_pieces(s, buf, bytes, dev::FixedProvL{1456, 0, 1456u}, n, dev::CrcEpi{out, uint32_t(n)}, nullptr); }, {}});
 
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
