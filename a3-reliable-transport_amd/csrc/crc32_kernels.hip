@@ -450,11 +450,25 @@ constexpr uint32_t kPcHinit = kPcOps + 5 * kOpBytes;
 constexpr uint32_t kPcStage = kPcHinit + 272;
 constexpr uint32_t kPcChunks = 272;  // span chunks a slot holds: 64 pieces + gaps + head slack
 constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read one chunk past
-constexpr uint32_t kPcLdsWords = (kPcStage + 16 * kPcSlot) / 4;  // 160,528 B
+constexpr uint32_t kPcFlags = kPcStage + 16 * kPcSlot;  // 64 B per wave: packet-start flags
+constexpr uint32_t kPcLdsWords = (kPcFlags + 16 * 64) / 4;  // 161,552 B
 static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
 static_assert(kPcLdsWords * 4 <= 163840, "LDS");
 
 __device__ __forceinline__ uint32_t stage_addr(uint32_t chunk) { return 16u * (chunk + (chunk >> 4)); }
+
+// Inclusive prefix sum over the wave with DPP (no LDS round trips): Hillis-Steele within
+// each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 / row_bcast:31 carry the row
+// totals into the rows above.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false));
+    return v;
+}
 
 // Lane-contiguous load of kPcChunks 16-B chunks starting at view offset b16 (16-aligned,
 // may be negative near the buffer start): 4 full wave instructions + 16 lanes of a
@@ -540,39 +554,38 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         }
         const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 64u;
         const uint32_t kr = k - (lane == 0 ? skip : 0u);  // pieces still to do
-        uint32_t incl = kr;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t u = __shfl_up(incl, d);
-            if (lane >= d) incl += u;
-        }
+        const uint32_t incl = wave_incl_add(kr);
+        const uint32_t excl = incl - kr;
         const uint32_t navail = __popcll(__ballot(have));  // packets of the wave left in view
+        const uint32_t covered = uint32_t(__builtin_amdgcn_readlane(int(incl), int(navail - 1)));  // pieces in view
 
-        // --- lane -> (packet, piece): pk = #packets whose pieces all precede this lane ---
-        uint32_t pk = 0;
-#pragma unroll
-        for (uint32_t s = 32; s >= 1; s >>= 1) {
-            const uint32_t probe = pk + s - 1;
-            const uint32_t v = __shfl(incl, probe & 63u);
-            if (probe < navail && v <= lane) pk += s;
-        }
-        const bool mapped = pk < navail;
+        // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
+        // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
+        uint8_t *flags = reinterpret_cast<uint8_t *>(lds + kPcFlags + wave * 64u);
+        flags[lane] = 0;
+        if (have && excl < 64u) flags[excl] = 1;
+        __builtin_amdgcn_wave_barrier();
+        const bool start = flags[lane] != 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t starts = __ballot(start);
+        uint32_t pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
+                      (start ? 1u : 0u) - 1u;
+        const bool mapped = lane < covered;
         pk = mapped ? pk : 0;
-        const uint32_t pinc = __shfl(incl, pk);
-        const uint32_t pkr = __shfl(kr, pk);
+        const uint32_t pex = __shfl(excl, pk);
         const uint32_t pkk = __shfl(k, pk);
         const uint32_t plen = __shfl(len, pk);
         const uint32_t poff = __shfl(uint32_t(off), pk);  // < 2^31: the view is < 2 GiB
         const bool pvalid = __shfl(valid ? 1u : 0u, pk) != 0;
         const uint32_t paux = __shfl(aux, pk);
-        const uint32_t lp = lane - (pinc - pkr);         // piece index within this round
+        const uint32_t lp = lane - pex;                  // piece index within this round
         const uint32_t gp = lp + (pk == 0 ? skip : 0u);  // piece index within the packet
 
         // --- piece window: the 64 bytes ending at this piece's end ----------------------
         const int32_t we = int32_t(poff + plen) - int32_t(pkk - 1 - gp) * kPieceS;
         const int32_t ws = we - kPieceS;
         // the round: lanes up to the first one whose window leaves [lo16, lo16 + span)
-        const int32_t lo16 = __builtin_amdgcn_readfirstlane(__shfl(ws, 0)) & ~15;
+        const int32_t lo16 = __builtin_amdgcn_readlane(ws, 0) & ~15;
         const bool out = !mapped || ws < lo16 || we - lo16 > kSpanBytes;
         const uint64_t outm = __ballot(out);
         const uint32_t total = outm ? uint32_t(__builtin_ctzll(outm)) : 64u;  // >= 1: lane 0 fits
@@ -609,10 +622,10 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 
         // --- round bookkeeping and the next round's prefetch ------------------------------
         const uint32_t tl = total - 1;
-        const uint32_t last_pk = __builtin_amdgcn_readfirstlane(__shfl(pk, tl));
-        const uint32_t last_gp = __builtin_amdgcn_readfirstlane(__shfl(gp, tl));
-        const uint32_t last_k = __builtin_amdgcn_readfirstlane(__shfl(pkk, tl));
-        const int32_t last_we = __builtin_amdgcn_readfirstlane(__shfl(we, tl));
+        const uint32_t last_pk = __builtin_amdgcn_readlane(pk, tl);
+        const uint32_t last_gp = __builtin_amdgcn_readlane(gp, tl);
+        const uint32_t last_k = __builtin_amdgcn_readlane(pkk, tl);
+        const int32_t last_we = __builtin_amdgcn_readlane(we, tl);
         const bool partial = last_gp + 1 < last_k;
         const uint64_t p0n = p0 + last_pk + (partial ? 0u : 1u);
         meta(p0n);  // first: the next round waits for these, not for the span
@@ -628,13 +641,18 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
 
         uint32_t c = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
+        const int32_t vf8 = 8 * vf;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
-            // keep bytes at window offset >= vf
-            const int32_t sh = vf - 4 * i;
-            const uint32_t keep = sh <= 0 ? 0xFFFFFFFFu : (sh >= 4 ? 0u : (0xFFFFFFFFu << (8 * sh)));
-            c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (wd & keep));
+            const uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
+            // keep the bytes at window offset >= vf: the low s = clamp(8 vf - 32 i, 0, 32)
+            // bits of word i go.  One v_med3 + one v_lshlrev_b64 (the shift unit reads 6
+            // bits: word 2j takes the low half of 0xFFFFFFFF << s, word 2j+1 the high half
+            // of 0xFFFFFFFF << (s + 32), and s = 32 wraps to a zero high half)
+            const int32_t t = vf8 < 32 * i ? 32 * i : (vf8 > 32 * i + 32 ? 32 * i + 32 : vf8);
+            const uint64_t k64 = uint64_t(0xFFFFFFFFu) << (uint32_t(t) & 63u);
+            const uint32_t keep = (i & 1) ? uint32_t(k64 >> 32) : uint32_t(k64);
+            c = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(c, wd, keep, 0x78));  // c ^ (wd & keep)
         }
         // head piece: R_~0(head) = R_0(0^vf || head) ^ shift(~0, 64 - vf)
         const uint32_t hw = lds_rd(lds, kPcHinit + 4u * uint32_t(kPieceS - (vf < 0 ? 0 : vf)));
@@ -652,7 +670,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
             if (lp >= dd && lane >= dd) W ^= op_apply(lds, kPcOps + o * kOpBytes, u);
         }
         epi.put(p0 + pk, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
-        carry = partial ? uint32_t(__shfl(W, tl)) : 0u;
+        carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
         skip = partial ? last_gp + 1 : 0u;
         p0 = p0n;
     }
