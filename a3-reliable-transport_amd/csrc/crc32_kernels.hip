@@ -59,12 +59,8 @@ constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..3
 constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
 constexpr uint32_t TAB_WORDS = OFF_HINIT + 68;
 
-// LDS images.  Replicated word tables: byte address
-//   t_hi*65536 + e*256 + t_lo*128 + (lane&31)*4   for table t = 2*t_hi + t_lo,
-// so a ds_read_b32 by lane L always lands in bank L%32 whatever the byte e.
-constexpr uint32_t kRepBytes = 131072;
-constexpr uint32_t kOpBytes = 4096;
-constexpr uint32_t kLdsWords = (kRepBytes + 6 * kOpBytes) / 4;  // 155,648 B (k_pieces)
+// LDS images (staggered table sets are described at StagKeys below).
+constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
 // k_fixed_braid: region A = {braid tables, x^-32}, region B = {x^-64, x^-128} (staggered,
 // conflict-free), then x^-256, x^-512, x^-1024 as plain 4 KiB operators.
 constexpr uint32_t kBraidPlainOps = 131072;
@@ -79,53 +75,14 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // also counts on lgkmcnt and serialises with the LDS lookups.
 typedef const __attribute__((address_space(1))) uint8_t gu8;
 typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+// Explicit LDS (address space 3) pointers for the general kernel's staging slots and
+// flags: the accesses are ds_* by construction, never flat.
+typedef __attribute__((address_space(3))) char lchar;
+typedef __attribute__((address_space(3))) u32x4 lu32x4;
+typedef __attribute__((address_space(3))) uint8_t lu8;
 
 __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
-}
-
-// Copy four 256-entry word tables from global into the replicated LDS image.
-__device__ __forceinline__ void fill_replicated(char *lds, const uint32_t *__restrict__ g) {
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
-        const uint32_t t = i >> 8, e = i & 255u;
-        const uint32_t v = g[i];
-        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + (t >> 1) * 65536u + e * 256u + (t & 1u) * 128u);
-        const u32x4 q = {v, v, v, v};
-#pragma unroll
-        for (int c = 0; c < 8; ++c) dst[c] = q;
-    }
-}
-
-__device__ __forceinline__ void fill_ops(char *lds, const uint32_t *__restrict__ g, int nops) {
-    u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kRepBytes);
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(g);
-    for (int i = threadIdx.x; i < nops * 256; i += blockDim.x) dst[i] = src[i];
-}
-
-// Per-lane address constants for the replicated tables: byte0 = t_lo<<7 | (lane&31)<<2,
-// byte2 = t_hi.  v_perm_b32(x, K_t, sel_t) = K_t.b0 | x.b_t << 8 | K_t.b2 << 16.
-struct RepKeys {
-    uint32_t k[4];
-    __device__ __forceinline__ explicit RepKeys(uint32_t lane) {
-        const uint32_t c4 = (lane & 31u) << 2;
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) k[t] = ((t & 1u) << 7) | c4 | ((t >> 1) << 16);
-    }
-};
-
-// XOR_t table_t[byte_t(x)] through the replicated image (4 v_perm + 4 ds_read_b32).
-__device__ __forceinline__ uint32_t rep_word(const char *lds, const RepKeys &K, uint32_t x) {
-    const uint32_t a0 = __builtin_amdgcn_perm(x, K.k[0], 0x0C020400u);
-    const uint32_t a1 = __builtin_amdgcn_perm(x, K.k[1], 0x0C020500u);
-    const uint32_t a2 = __builtin_amdgcn_perm(x, K.k[2], 0x0C020600u);
-    const uint32_t a3 = __builtin_amdgcn_perm(x, K.k[3], 0x0C020700u);
-    return (lds_rd(lds, a0) ^ lds_rd(lds, a1)) ^ (lds_rd(lds, a2) ^ lds_rd(lds, a3));
-}
-
-// Table 3 of the slice-by-4 set is the plain Sarwate table: one byte step.
-__device__ __forceinline__ uint32_t rep_byte(const char *lds, const RepKeys &K, uint32_t c, uint32_t b) {
-    const uint32_t a = __builtin_amdgcn_perm((c ^ b), K.k[3], 0x0C020400u);
-    return lds_rd(lds, a) ^ (c >> 8);
 }
 
 // Linear operator stored as 4 byte tables at LDS byte offset `base`.
@@ -236,10 +193,56 @@ __device__ __forceinline__ uint32_t stag_apply3(const char *lds, const uint32_t 
 
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by a
 // plain XOR, bit1 skips the combine.  Production instantiations use DIAG = 0.
-template <int ROWS, int FRAME = kBraidFrame, int DIAG = 0, int DEPTH = kBraidDepth>
+// Epilogues of the braided kernel.  A flush hands lane 4k + q the result of packet
+// slot q of the k-th round of its 16-round group; pre() issues, one group ahead, the
+// loads put() will need (so a flush never waits on memory).
+struct CrcBEpi {  // out[p] = crc
+    uint32_t *out;
+    uint32_t cinit;  // init_const(len)
+    struct Pre {};
+    __device__ __forceinline__ void pre(uint64_t, Pre &) const {}
+    __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
+        if (on) out[p] = v ^ cinit;
+    }
+};
+// Receiver verify over a datagram ring with payloads [16, stride): the kernel runs on
+// base = ring + 16, len = stride - 16.  Full datagrams (recv_len == stride) are
+// decided here (Receiver.cpp:203-206: ntohl(header.checksum) == crc32(payload));
+// every other datagram goes to the fix-up list, which the general kernel finishes.
+struct VerifyBEpi {
+    const uint32_t *rl;
+    const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
+    uint64_t stride;
+    uint8_t *ok;
+    uint32_t *crc;  // may be null
+    uint32_t *fix;  // fix[0] = count, fix[1..] = datagram indices
+    uint32_t cinit;
+    uint64_t n;
+    struct Pre {
+        uint32_t r, h;
+    };
+    __device__ __forceinline__ void pre(uint64_t p, Pre &q) const {
+        typedef const __attribute__((address_space(1))) uint32_t gu32;
+        const uint64_t pc = p < n ? p : n - 1;
+        q.r = ((gu32 *)rl)[pc];
+        q.h = *(gu32 *)((gu8 *)ring + pc * stride + 12);
+    }
+    __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &q) const {
+        if (!on) return;
+        if (q.r == uint32_t(stride)) {
+            const uint32_t c = v ^ cinit;
+            ok[p] = bswap32(q.h) == c ? 1 : 0;
+            if (crc) crc[p] = c;
+        } else {
+            fix[1 + atomicAdd(fix, 1u)] = uint32_t(p);
+        }
+    }
+};
+
+template <int ROWS, int FRAME = kBraidFrame, int DIAG = 0, int DEPTH = kBraidDepth, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
-                                                      uint32_t len, uint64_t n, uint32_t *__restrict__ out,
-                                                      const uint32_t *__restrict__ gtab, uint32_t cinit) {
+                                                      uint32_t len, uint64_t n, BEpi epi,
+                                                      const uint32_t *__restrict__ gtab) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
 
@@ -287,8 +290,11 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     uint32_t col = 0, colt = 0;  // collected results / trails, slot 4k + q
     uint32_t k = 0;              // rounds collected since the last flush
     uint64_t rfirst = 0;         // round of slot group 0
+    typename BEpi::Pre pre{};    // epilogue loads for the current group
+    // packet of lane 4k + q in the group starting at round g0
+    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 2) * rstep) * 4 + (lane & 3u); };
 
-    auto flush = [&]() {
+    auto flush = [&](uint64_t next_g0, bool more) {
         const uint32_t t = colt >> 4;  // x^(-8T), T = 16t
         uint32_t v = col;
         if (t & 1u) v = stag_apply3<128>(lds, K.kB, K.sel, v);  // x^-128
@@ -297,7 +303,8 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
         if (t & 8u) v = inv_plain(2, v);                        // x^-1024
         const uint64_t rr = rfirst + uint64_t(lane >> 2) * rstep;
         const uint64_t p = rr * 4 + (lane & 3u);
-        if ((lane >> 2) < k && rr < rounds && p < n) out[p] = v ^ cinit;
+        epi.put(p, v, (lane >> 2) < k && rr < rounds && p < n, pre);
+        if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
     };
 
@@ -348,12 +355,13 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             col = mv;
             colt = mt;
         }
-        if (++k == 16) flush();
+        if (++k == 16) flush(rr + rstep, true);
     };
 
     uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B, C;
+    epi.pre(group_packet(r), pre);
     load_round(r, A);
     if (DEPTH == 2) load_round(r + rstep, B);
     fill_stag(lds, 0, 0, gtab + OFF_BRAID);
@@ -392,7 +400,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             r += rstep;
         }
     }
-    if (k) flush();
+    if (k) flush(0, false);
 }
 
 // ------------------------------------------------------------------------------------
@@ -508,6 +516,11 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
                                                  uint32_t *__restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
+    n = prov.count(n);  // device-side count for the fix-up pass
+    {
+        const uint64_t tw = uint64_t(gridDim.x) * (blockDim.x >> 6), w0 = uint64_t(blockIdx.x) * (blockDim.x >> 6);
+        if (n * w0 / tw == n * (w0 + (blockDim.x >> 6)) / tw) return;  // no packets for this block
+    }
     fill_stag(lds, 0, 0, gtab + OFF_S4);
     fill_stag(lds, 0, 1, gtab + OFF_FWD);
     {
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     const uint64_t lo = n * gw / tw, hi = n * (gw + 1) / tw;
     const StagKeys K(lane);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
-    char *slot = lds + kPcStage + wave * kPcSlot;
+    lchar *const slot = (lchar *)lds_w + kPcStage + wave * kPcSlot;
     constexpr int32_t kSpanBytes = int32_t(16 * kPcChunks);
     constexpr int32_t kNoSpan = 0x7FFFF000;  // out of range: loads return 0, no traffic
 
@@ -543,9 +556,9 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     u32x4 x[5];
     for (uint64_t p0 = lo; p0 < hi;) {
         uint64_t off;
-        uint32_t len, aux = 0;
+        uint32_t len, aux = 0, oslot = 0;
         bool valid;
-        prov.decode(raw, off, len, valid, aux);
+        prov.decode(raw, off, len, valid, aux, oslot);
         const bool have = p0 + lane < hi;
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 
         // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
         // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
-        uint8_t *flags = reinterpret_cast<uint8_t *>(lds + kPcFlags + wave * 64u);
+        lu8 *const flags = (lu8 *)lds_w + kPcFlags + wave * 64u;
         flags[lane] = 0;
         if (have && excl < 64u) flags[excl] = 1;
         __builtin_amdgcn_wave_barrier();
@@ -578,6 +591,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         const uint32_t poff = __shfl(uint32_t(off), pk);  // < 2^31: the view is < 2 GiB
         const bool pvalid = __shfl(valid ? 1u : 0u, pk) != 0;
         const uint32_t paux = __shfl(aux, pk);
+        const uint64_t pout = Prov::kIndexed ? uint64_t(uint32_t(__shfl(oslot, pk))) : p0 + pk;  // output index
         const uint32_t lp = lane - pex;                  // piece index within this round
         const uint32_t gp = lp + (pk == 0 ? skip : 0u);  // piece index within the packet
 
@@ -603,15 +617,15 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the miss pays its latency here
         }
 #pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) *reinterpret_cast<u32x4 *>(slot + stage_addr(64u * i + lane)) = x[i];
-        if (lane < kPcChunks - 256u) *reinterpret_cast<u32x4 *>(slot + stage_addr(256u + lane)) = x[4];
+        for (uint32_t i = 0; i < 4; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
+        if (lane < kPcChunks - 256u) *(lu32x4 *)(slot + stage_addr(256u + lane)) = x[4];
         __builtin_amdgcn_wave_barrier();
         uint32_t d[20];
         {
             const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
 #pragma unroll
             for (uint32_t u = 0; u < 5; ++u) {
-                const u32x4 y = *reinterpret_cast<const u32x4 *>(slot + stage_addr(blk + u));
+                const u32x4 y = *(const lu32x4 *)(slot + stage_addr(blk + u));
                 d[4 * u + 0] = y.x;
                 d[4 * u + 1] = y.y;
                 d[4 * u + 2] = y.z;
@@ -669,7 +683,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
             const uint32_t u = __shfl_up(W, dd);
             if (lp >= dd && lane >= dd) W ^= op_apply(lds, kPcOps + o * kOpBytes, u);
         }
-        epi.put(p0 + pk, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
+        epi.put(pout, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
         carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
         skip = partial ? last_gp + 1 : 0u;
         p0 = p0n;
@@ -802,7 +816,7 @@ int init_device(int dev) {
             s.err = m;
         };
         int prev = 0;
-        hipGetDevice(&prev);
+        (void)hipGetDevice(&prev);
         if (hipSetDevice(dev) != hipSuccess) return setfail(WTP_ENODEV, "hipSetDevice failed");
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return setfail(WTP_ENODEV, "hipGetDeviceProperties failed");
@@ -815,7 +829,7 @@ int init_device(int dev) {
             return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
         if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
         if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
-        hipSetDevice(prev);
+        (void)hipSetDevice(prev);
     });
     if (s.rc != WTP_OK) return fail(s.rc, "wtp init(device %d): %s", dev, s.err.c_str());
     return WTP_OK;
@@ -836,27 +850,30 @@ int launch_check(const char *what) {
     return WTP_OK;
 }
 
-template <int ROWS>
+template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len, uint64_t n,
-                       uint32_t *out, const uint32_t *tabs, uint32_t cinit) {
-    hipLaunchKernelGGL(dev::k_fixed_braid<ROWS>, grid, dim3(1024), 0, st, b, uint32_t(stride), len, n, out, tabs,
-                       cinit);
+                       BEpi epi, const uint32_t *tabs) {
+    hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, dev::kBraidFrame, 0, dev::kBraidDepth, BEpi>), grid, dim3(1024), 0, st, b,
+                       uint32_t(stride), len, n, epi, tabs);
 }
 
-int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
-                       uint32_t *out, hipStream_t st) {
+// Braided kernel over n packets base[p*stride, +len): base, stride, len multiples of 16,
+// 16 <= len <= 1536, stride <= 16 KiB.  The epilogue's cinit is filled in here.
+template <class BEpi>
+int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
+                       hipStream_t st) {
     const int rows = int((len + 255) / 256);
     const uint64_t rounds = (n + 3) / 4;
     const uint64_t want = (rounds + 15) / 16;
     const unsigned grid = unsigned(want < uint64_t(s.cus) ? want : uint64_t(s.cus));
-    const uint32_t cinit = init_const(len);
+    epi.cinit = init_const(len);
     switch (rows) {
-        case 1: launch_braid_rows<1>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
-        case 2: launch_braid_rows<2>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
-        case 3: launch_braid_rows<3>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
-        case 4: launch_braid_rows<4>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
-        case 5: launch_braid_rows<5>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
-        case 6: launch_braid_rows<6>(grid, st, base, stride, len, n, out, s.tabs, cinit); break;
+        case 1: launch_braid_rows<1>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 2: launch_braid_rows<2>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 3: launch_braid_rows<3>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 4: launch_braid_rows<4>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 5: launch_braid_rows<5>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 6: launch_braid_rows<6>(grid, st, base, stride, len, n, epi, s.tabs); break;
         default: return fail(WTP_EINVAL, "braid rows %d", rows);
     }
     return launch_check("k_fixed_braid");
@@ -888,26 +905,33 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
 namespace dev {
 // Providers split metadata access in two: load() only issues loads (its results are
 // consumed a round later, so no arithmetic may touch them there) and decode() turns the
-// raw words into (offset in the view, length, valid, aux) when the round uses them.
+// raw words into (offset in the view, length, valid, aux, output slot) when the round
+// uses them.  count(n) is the number of packets (device-side for the fix-up pass).
 struct FixedProvL {
+    static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     uint32_t len;
+    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
-    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &) const {
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
+                                           uint32_t &) const {
         off = lead + r.a * stride;
         l = len;
         ok = true;
     }
 };
 struct ArrayProvL {
+    static constexpr bool kIndexed = false;
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
+    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
         r.a = reinterpret_cast<const uint32_t *>(offs)[2 * p];  // low dword: the view is < 2 GiB
         r.b = lens[p];
     }
-    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &) const {
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
+                                           uint32_t &) const {
         off = lead + r.a;
         l = r.b;
         ok = true;
@@ -919,8 +943,10 @@ struct ArrayProvL {
 // the last datagram, reads there return 0 and are never selected) and are
 // funnel-shifted at decode.
 struct DgramProvL {
+    static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
+    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
         const uint32_t h = uint32_t(lead + p * stride + 12) & ~3u;  // the view is < 2 GiB
         r.a = p;
@@ -929,13 +955,44 @@ struct DgramProvL {
         r.c = w.x;
         r.d = w.y;
     }
-    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok,
-                                           uint32_t &want) const {
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
+                                           uint32_t &) const {
         const uint64_t d = lead + r.a * stride;
         want = bswap32(__builtin_amdgcn_alignbyte(r.d, r.c, uint32_t(d + 12) & 3u));
         off = d + 16;
         ok = r.b >= 16 && r.b <= stride;
         l = ok ? r.b - 16 : 0;
+    }
+};
+// The fix-up pass of the braided verify: datagrams fix[1 .. fix[0]] of the ring (in
+// whatever order the atomics left them).  The index load makes this provider's other
+// loads dependent (it only sees the rare short or malformed datagrams).
+struct IdxDgramProvL {
+    static constexpr bool kIndexed = true;
+    uint64_t stride, lead;
+    const uint32_t *__restrict__ rl;
+    const uint32_t *__restrict__ fix;
+    __device__ __forceinline__ uint64_t count(uint64_t n) const {
+        const uint64_t c = *(const __attribute__((address_space(1))) uint32_t *)fix;  // written by the braid pass
+        return c < n ? c : n;
+    }
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
+        const uint32_t idx = fix[1 + p];
+        const uint32_t h = uint32_t(lead + uint64_t(idx) * stride + 12) & ~3u;
+        r.a = idx;
+        r.b = rl[idx];
+        const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(h), 0, 0));
+        r.c = w.x;
+        r.d = w.y;
+    }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
+                                           uint32_t &slot) const {
+        const uint64_t d = lead + r.a * stride;
+        want = bswap32(__builtin_amdgcn_alignbyte(r.d, r.c, uint32_t(d + 12) & 3u));
+        off = d + 16;
+        ok = r.b >= 16 && r.b <= stride;
+        l = ok ? r.b - 16 : 0;
+        slot = uint32_t(r.a);
     }
 };
 }  // namespace dev
@@ -998,7 +1055,7 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
     // inside the 74 KB table buffer used as the dead-round prefetch target
     const bool fast = len >= 16 && len <= 1536 && len % 16 == 0 && stride % 16 == 0 && stride <= 16384 &&
                       reinterpret_cast<uintptr_t>(b) % 16 == 0;
-    if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, d_out, st);
+    if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, dev::CrcBEpi{d_out, 0}, st);
     // general kernel, in sub-batches whose byte span stays < 2 GiB
     const uint64_t per = std::min<uint64_t>(kSubBatch, stride ? std::max<uint64_t>(1, ((1ull << 30) - 4096) / stride) : n);
     for (uint64_t p = 0; p < n; p += per) {
@@ -1039,15 +1096,43 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     DevState *s = nullptr;
     int rc = current(s);
     if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t *b = static_cast<const uint8_t *>(d_dgrams);
+    // Braided fast path for a 16-B aligned ring whose full datagrams fit one braid frame
+    // (e.g. stride 1472 = header + 1456): it decides every full datagram; the rest
+    // (short, empty or malformed) are listed on the device and the general kernel
+    // finishes them, reading its packet count from the list.
+    if (stride % 16 == 0 && stride >= 32 && stride <= 1552 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
+        const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
+        uint32_t *fix = nullptr;
+        WTP_HIP(hipMallocAsync(reinterpret_cast<void **>(&fix), 4 * (std::min<uint64_t>(per, n) + 1), st));
+        for (uint64_t p = 0; p < n && !rc; p += per) {
+            const uint64_t cnt = std::min<uint64_t>(per, n - p);
+            const uint8_t *sb = b + p * stride;
+            uint8_t *ok = d_ok + p;
+            uint32_t *crc = d_crc_out ? d_crc_out + p : nullptr;
+            if (hipMemsetAsync(fix, 0, 4, st) != hipSuccess) {
+                rc = fail(WTP_EHIP, "hipMemsetAsync failed");
+                break;
+            }
+            rc = launch_fixed_braid(*s, sb + 16, stride, uint32_t(stride - 16), cnt,
+                                    dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt}, st);
+            if (!rc)
+                rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix}, cnt,
+                                   dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);
+        }
+        const hipError_t fe = hipFreeAsync(fix, st);
+        if (rc) return rc;
+        if (fe != hipSuccess) return fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
+        return WTP_OK;
+    }
     const uint64_t per = std::min<uint64_t>(kSubBatch, std::max<uint64_t>(1, (1ull << 30) / stride));
     for (uint64_t p = 0; p < n; p += per) {
         const uint64_t cnt = std::min<uint64_t>(per, n - p);
         const uint8_t *sb = b + p * stride;
         const uint64_t lead = reinterpret_cast<uintptr_t>(sb) & 15u;
         rc = launch_pieces(*s, sb, cnt * stride, dev::DgramProvL{stride, lead, d_recv_len + p}, cnt,
-                           dev::VerifyEpi{d_ok + p, d_crc_out ? d_crc_out + p : nullptr, uint32_t(cnt)},
-                           static_cast<hipStream_t>(stream));
+                           dev::VerifyEpi{d_ok + p, d_crc_out ? d_crc_out + p : nullptr, uint32_t(cnt)}, st);
         if (rc) return rc;
     }
     return WTP_OK;
@@ -1078,7 +1163,7 @@ int wtp_build_data_packets(const void *d_payloads, size_t total_bytes, uint32_t 
     if (!crc) {
         std::lock_guard<std::mutex> g(s->scratch_mu);
         if (s->scratch_words < nch) {
-            if (s->scratch) hipFree(s->scratch);
+            if (s->scratch) (void)hipFree(s->scratch);
             s->scratch = nullptr;
             s->scratch_words = 0;
             WTP_HIP(hipMalloc(&s->scratch, nch * 4));

@@ -69,8 +69,9 @@ int wtp_device_count(void);
    lazily on first use).  Call before capturing a launch into a hipGraph. */
 int wtp_init(int device);
 
-/* Sticky device-side data-error flags of `device` (bit 0: a payload length was
-   > WTP_MAX_PAYLOAD).  Synchronous; clears the flags when `clear` != 0. */
+/* Sticky device-side data-error flags of `device` (bit 0: a general-kernel payload
+   length was > WTP_MAX_KERNEL_LEN; that payload's result is then 0 / not ok).
+   Synchronous; clears the flags when `clear` != 0. */
 int wtp_device_status(int device, uint32_t *flags, int clear);
 
 /* ---- CPU reference semantics (single packet) --------------------------------------
@@ -83,22 +84,28 @@ uint32_t wtp_crc32(const void *buf, size_t size);
    Sender packet build, batched: payload i = d_payloads[i*stride .. i*stride+len).
    Replaces the per-chunk crc32 of Packet(DATA, chunk, seq) in the send loop
    (cpp/src/base/Sender.cpp:88-95 -> Packet.cpp:13).  Fast path (braided CDNA4
-   kernel): base % 16 == 0, stride % 16 == 0, len % 16 == 0, 16 <= len <= 1536;
-   other shapes run the general kernel. */
+   kernel): base % 16 == 0, stride % 16 == 0, len % 16 == 0, 16 <= len <= 1536,
+   stride <= 16384; other shapes run the general kernel (len <= WTP_MAX_KERNEL_LEN). */
 int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, size_t n,
                           uint32_t *d_out, void *stream);
 
 /* Mixed lengths: payload i = d_base[d_offsets[i] .. d_offsets[i] + d_lengths[i]).
-   `base_bytes` = size of the d_base buffer (bounds for the loads). */
+   `base_bytes` = size of the d_base buffer (bounds for the loads; < 2 GiB, so only
+   the low 32 bits of each offset are read).  d_lengths[i] <= WTP_MAX_KERNEL_LEN. */
 int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                         const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
 /* Receiver verify, batched (cpp/src/base/Receiver.cpp:25-35 + :203-206): datagram i is
    d_dgrams[i*stride .. i*stride + d_recv_len[i]) = 16-B big-endian PacketHeader ||
    payload.  As in the reference, the CRC covers bytes [16, recv_len) and
-   header.length is ignored.  d_ok[i] = 1 iff recv_len >= 16 and
-   ntohl(header.checksum) == crc32(payload), else 0 (drop, no ACK).  d_crc_out may be
-   NULL; otherwise it receives the computed CRCs (0 for runts). */
+   header.length is ignored.  d_ok[i] = 1 iff 16 <= recv_len <= stride and
+   ntohl(header.checksum) == crc32(payload), else 0 (drop, no ACK).  A recv_len
+   above stride (more than the ring slot holds; recvfrom cannot return it) is
+   malformed: ok 0.  d_crc_out may be NULL; otherwise it receives the computed CRCs
+   (0 for runts and malformed lengths).  Fast path: a 16-B aligned ring with
+   stride % 16 == 0 and stride <= 1552 (e.g. 1472 = header + 1456) runs the braided
+   kernel over every slot's full payload and finishes the datagrams with
+   recv_len != stride in a second, general-kernel pass. */
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len,
                            size_t n, uint8_t *d_ok, uint32_t *d_crc_out, void *stream);
 

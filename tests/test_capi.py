@@ -42,6 +42,32 @@ def test_library_has_gfx950_code_object():
     assert b"gfx950" in blob
 
 
+def _gfx950_disassembly(lib_path, tmp_path):
+    llvm = "/opt/rocm/lib/llvm/bin"
+    fb, co = str(tmp_path / "fatbin"), str(tmp_path / "k.co")
+    # -O binary with an explicit output file: objcopy never touches (rewrites) the library
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib_path, fb], check=True,
+                   capture_output=True)
+    subprocess.run([llvm + "/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fb,
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True, capture_output=True)
+    return subprocess.run([llvm + "/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+                          text=True).stdout
+
+
+def test_kernels_use_no_flat_memory_ops(tmp_path):
+    """Every kernel reaches memory through global/buffer (HBM) or ds (LDS) instructions.
+    A flat op means the compiler lost a pointer's address space: flat ops count on both
+    vmcnt and lgkmcnt (serialising loads with the LDS table lookups), and once one was
+    emitted on a bare LDS offset, i.e. an illegal global address."""
+    import wtp_crc32 as W
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("no ROCm llvm tools")
+    dis = _gfx950_disassembly(W.LIB_PATH, tmp_path)
+    assert re.search(r"\bds_read_b128\b", dis) and re.search(r"\bbuffer_load_dwordx4\b", dis)
+    flat = [l.strip() for l in dis.splitlines() if re.search(r"\bflat_\w+", l)]
+    assert not flat, flat[:5]
+
+
 def test_cpu_crc32_golden(golden):
     import wtp_crc32 as W
     assert W.crc32(b"123456789") == 0xCBF43926

@@ -222,6 +222,102 @@ def test_verify_batch(W):
     assert want_ok.sum() < n - 200  # the corruptions were caught
 
 
+def _full_ring(n, stride, rng, frac_full=0.9):
+    """A receive ring as the braided verify path sees it: mostly full datagrams
+    (recv_len == stride), the rest short, empty, runt or oversize."""
+    L = stride - 16
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    rl = np.zeros(n, dtype=np.uint32)
+    body = O.synth_fill_np(n * L, start_byte=stride)
+    for i in range(n):
+        u = rng.random()
+        if u < frac_full:
+            p = body[i * L:(i + 1) * L].tobytes()
+        else:
+            p = body[i * L:i * L + int(rng.integers(0, L))].tobytes()
+        dg = O.build_datagram(i, p)
+        buf[i * stride:i * stride + len(dg)] = np.frombuffer(dg, dtype=np.uint8)
+        rl[i] = len(dg)
+    k = max(1, n // 50)
+    idx = rng.choice(n, 4 * k, replace=False)
+    for i in idx[:k]:  # payload bit flips
+        if rl[i] > 16:
+            buf[i * stride + 16 + int(rng.integers(0, rl[i] - 16))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    for i in idx[k:2 * k]:  # header checksum flips
+        buf[i * stride + 12 + int(rng.integers(0, 4))] ^= 0x10
+    rl[idx[2 * k:3 * k]] = rng.integers(0, 16, k).astype(np.uint32)  # runts
+    rl[idx[3 * k:]] = stride + rng.integers(1, 40, k).astype(np.uint32)  # oversize (truncated)
+    return buf, rl
+
+
+def _verify_dev(W, buf, stride, rl, n, with_crc=True, offset=0):
+    raw = np.zeros(len(buf) + offset, dtype=np.uint8)
+    raw[offset:] = buf
+    d = dev_u8(raw)[offset:]
+    r = torch.from_numpy(rl.view(np.int32)).cuda()
+    ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    crc = u32_out(n) if with_crc else None
+    W.verify_batch(d, stride, r, n, ok, crc)
+    torch.cuda.synchronize()
+    return ok.cpu().numpy(), (to_u32(crc, n) if with_crc else None)
+
+
+@pytest.mark.parametrize("n,stride,frac,with_crc", [
+    (3001, 1472, 0.9, True),    # braided fast path + fix-up list
+    (3001, 1472, 0.9, False),   # no crc output
+    (517, 1472, 1.0, True),     # every datagram full
+    (400, 1488, 0.0, True),     # 16-B stride, no datagram full: all through the fix-up
+    (999, 32, 0.7, True),       # smallest fast-path stride (16-B payloads)
+    (777, 1104, 0.8, True),     # 4-row braid frames
+])
+def test_verify_fast_path(W, n, stride, frac, with_crc):
+    rng = np.random.default_rng(n + stride)
+    buf, rl = _full_ring(n, stride, rng, frac)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    ok, crc = _verify_dev(W, buf, stride, rl, n, with_crc)
+    assert np.array_equal(ok, want_ok), np.nonzero(ok != want_ok)[0][:10]
+    if with_crc:
+        assert np.array_equal(crc, want_crc), np.nonzero(crc != want_crc)[0][:10]
+    assert 0 < want_ok.sum() < n or frac == 1.0 or frac == 0.0
+
+
+def test_verify_misaligned_ring_takes_general_path(W):
+    rng = np.random.default_rng(11)
+    n, stride = 700, 1472
+    buf, rl = _full_ring(n, stride, rng)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    ok, crc = _verify_dev(W, buf, stride, rl, n, True, offset=4)
+    assert np.array_equal(ok, want_ok) and np.array_equal(crc, want_crc)
+
+
+def test_verify_large_ring_properties(W):
+    """1M full 1472-B datagrams built on the device: every one verifies; one flipped
+    payload bit per 4099 datagrams is caught exactly there; sampled CRCs vs oracle."""
+    n, stride = 1 << 20, 1472
+    payload = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(payload)
+    wire = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    wl = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)
+    del payload
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    crc = u32_out(n)
+    W.verify_batch(wire, stride, wl, n, ok, crc)
+    torch.cuda.synchronize()
+    assert int(ok.sum().item()) == n
+    got = to_u32(crc, n)
+    for i in (0, 1, 2, 3, 4, 65535, n // 2 + 1, n - 2, n - 1):
+        assert int(got[i]) == O.crc32(O.synth_fill_np(1456, start_byte=i * 1456)), i
+    bad = torch.arange(0, n, 4099, device="cuda")
+    pos = bad * stride + 16 + (bad % 1456)
+    wire[pos] = wire[pos] ^ 1
+    ok.zero_()
+    W.verify_batch(wire, stride, wl, n, ok, None)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy()
+    assert set(np.nonzero(okh == 0)[0].tolist()) == set(bad.cpu().numpy().tolist())
+
+
 def test_host_verify(W):
     rng = np.random.default_rng(4)
     n, stride = 500, 1472

@@ -7,6 +7,7 @@
 //   braid_nocomb : production lookups, the x^-k folds and cross-lane tree removed
 // Output: one line per variant with median/min time and GB/s on 1M x 1456 B.
 #include "../a3-reliable-transport_amd/csrc/crc32_kernels.hip"
+#include "kbench_legacy.hpp"
 
 #include <algorithm>
 #include <cstdio>
@@ -298,14 +299,14 @@ int main(int argc, char **argv) {
     vs.push_back({"read_probe_g256x1024", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(1024), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
-    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"new_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"new_nocomb_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"new_nolut", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"new_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"new_nolut_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, out, s.tabs, cinit); }, {}});
+    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"new_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"new_nocomb_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"new_nolut", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"new_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"new_nolut_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
     vs.push_back({"braid_old_rightaligned", [&] { hipLaunchKernelGGL((k_braid_diag<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
     vs.push_back({"braid_nolut", [&] { hipLaunchKernelGGL((k_braid_diag<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
     vs.push_back({"braid_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});

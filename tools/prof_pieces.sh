@@ -1,0 +1,21 @@
+#!/usr/bin/env bash
+# SQ counter passes (one rocprofv3 --pmc run each, kernel trace only) over the general
+# kernel; output under gpurun_out/<tag>/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT="$(pwd)"; TAG="${1:-pp}"; OUT="$ROOT/gpurun_out/$TAG"; mkdir -p "$OUT"; export TMPDIR=/tmp
+cd /tmp
+i=0
+while read -r counters; do
+  [ -z "$counters" ] && continue
+  i=$((i+1))
+  echo "[$(date +%T)] pass $i: $counters"
+  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d "$OUT/p$i" -o pp -- python3 "$ROOT/tools/prof_pieces.py" 3 > "$OUT/p$i.log" 2>&1
+  rc=$?; echo "  rc=$rc"
+  case $rc in 0) ;; *) tail -5 "$OUT/p$i.log"; echo FATAL; exit $rc;; esac
+done <<'LIST'
+SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVES
+SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL GRBM_GUI_ACTIVE SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INST_LEVEL_LDS
+LIST
+echo done
