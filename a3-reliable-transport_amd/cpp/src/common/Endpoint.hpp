@@ -5,6 +5,7 @@
 // crc32() of Crc32.hpp (--crc cpu, the reference's behaviour).
 #pragma once
 
+#include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <sys/time.h>
@@ -99,8 +100,90 @@ class Checksums {
         return get_header(dgram).checksum == crc32(dgram + kHeaderBytes, len - kHeaderBytes);
     }
 
+    // Batched receiver verify: datagram i = ring[i*stride, +rl[i]).
+    // GPU mode verifies the whole batch in one call (the ring is pinned, so the library
+    // copies it to the device with one DMA); CPU mode is one crc32() per datagram.
+    void verify_batch(const uint8_t *ring, size_t stride, const uint32_t *rl, size_t n, uint8_t *ok) const {
+        if (!n) return;
+        if (gpu_) {
+            if (wtp_crc32_host_verify(ring, stride, rl, n, ok, nullptr) != WTP_OK)
+                throw std::runtime_error(std::string("wtp_crc32_host_verify: ") + wtp_last_error());
+            return;
+        }
+        for (size_t i = 0; i < n; ++i) {
+            const uint8_t *d = ring + i * stride;
+            ok[i] = rl[i] >= kHeaderBytes && rl[i] <= stride &&
+                    get_header(d).checksum == crc32(d + kHeaderBytes, rl[i] - kHeaderBytes);
+        }
+    }
+
    private:
     bool gpu_;
+};
+
+// Receive ring for recvmmsg: `slots` datagram slots of kSlot = header + max payload
+// bytes in pinned host memory (wtp_host_alloc), filled by one recvmmsg call per batch.
+// A datagram longer than a slot is truncated by the kernel; its length is then
+// reported as kSlot + 1 so that verify rejects it (the reference reads into a 1500-B
+// buffer and would CRC the truncated bytes; WTP datagrams never exceed 1472 B).
+class RecvRing {
+   public:
+    static constexpr size_t kSlot = kHeaderBytes + kMaxPayload;  // 1472
+    // pinned: allocate the ring with wtp_host_alloc (GPU verify: one DMA per batch);
+    // otherwise plain page-aligned memory (CPU verify needs no device).
+    RecvRing(size_t slots, bool pinned)
+        : n_(slots), pinned_(pinned),
+          buf_(static_cast<uint8_t *>(pinned ? wtp_host_alloc(slots * kSlot) : std::aligned_alloc(4096, round4k(slots * kSlot)))),
+          len_(slots), ok_(slots), iov_(slots), msg_(slots), peer_(slots) {
+        if (!buf_) throw std::runtime_error("receive ring allocation failed");
+        for (size_t i = 0; i < n_; ++i) {
+            iov_[i] = {buf_ + i * kSlot, kSlot};
+            msg_[i].msg_hdr.msg_iov = &iov_[i];
+            msg_[i].msg_hdr.msg_iovlen = 1;
+        }
+    }
+    ~RecvRing() {
+        if (pinned_)
+            wtp_host_free(buf_);
+        else
+            std::free(buf_);
+    }
+    RecvRing(const RecvRing &) = delete;
+    RecvRing &operator=(const RecvRing &) = delete;
+
+    // Block for at least one datagram, take up to `slots` (MSG_WAITFORONE).  Returns the
+    // count; 0 on timeout (SO_RCVTIMEO) or EINTR.
+    size_t receive(int fd) {
+        for (size_t i = 0; i < n_; ++i) {
+            msg_[i].msg_hdr.msg_name = &peer_[i];
+            msg_[i].msg_hdr.msg_namelen = sizeof(sockaddr_in);
+            msg_[i].msg_hdr.msg_flags = 0;
+        }
+        const int got = ::recvmmsg(fd, msg_.data(), unsigned(n_), MSG_WAITFORONE, nullptr);
+        if (got <= 0) return 0;
+        for (int i = 0; i < got; ++i) {
+            const bool trunc = (msg_[i].msg_hdr.msg_flags & MSG_TRUNC) != 0;
+            len_[i] = trunc ? uint32_t(kSlot + 1) : uint32_t(msg_[i].msg_len);
+        }
+        return size_t(got);
+    }
+    uint8_t *slot(size_t i) { return buf_ + i * kSlot; }
+    uint32_t len(size_t i) const { return len_[i]; }
+    const uint32_t *lens() const { return len_.data(); }
+    uint8_t *ok() { return ok_.data(); }
+    const sockaddr_in &peer(size_t i) const { return peer_[i]; }
+    uint8_t *ring() { return buf_; }
+
+   private:
+    static size_t round4k(size_t b) { return (b + 4095) & ~size_t(4095); }
+    size_t n_;
+    bool pinned_;
+    uint8_t *buf_;
+    std::vector<uint32_t> len_;
+    std::vector<uint8_t> ok_;
+    std::vector<iovec> iov_;
+    std::vector<mmsghdr> msg_;
+    std::vector<sockaddr_in> peer_;
 };
 
 inline int udp_socket() {

@@ -197,6 +197,7 @@ __device__ __forceinline__ uint32_t stag_apply3(const char *lds, const uint32_t 
 // slot q of the k-th round of its 16-round group; pre() issues, one group ahead, the
 // loads put() will need (so a flush never waits on memory).
 struct CrcBEpi {  // out[p] = crc
+    static constexpr bool kCopy = false;  // see BuildBEpi
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
     struct Pre {};
@@ -210,6 +211,7 @@ struct CrcBEpi {  // out[p] = crc
 // decided here (Receiver.cpp:203-206: ntohl(header.checksum) == crc32(payload));
 // every other datagram goes to the fix-up list, which the general kernel finishes.
 struct VerifyBEpi {
+    static constexpr bool kCopy = false;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
     uint64_t stride;
@@ -236,6 +238,39 @@ struct VerifyBEpi {
         } else {
             fix[1 + atomicAdd(fix, 1u)] = uint32_t(p);
         }
+    }
+};
+
+// Fused DATA packet builder (Packet.cpp:9-14,40-47,
+// Sender.cpp:187-197): payload p (stride len) -> wire[p*wstride ..) = big-endian
+// PacketHeader{DATA, seq0 + p, len, crc} || payload.  kCopy: every 16-B chunk the
+// kernel loads is also stored into its wire slot in the same round (one buffer store
+// per row, out-of-range offset for chunks outside the packet), so the payload is read
+// from HBM once; the header follows at the flush.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes);
+struct BuildBEpi {
+    static constexpr bool kCopy = true;
+    uint8_t *wire;
+    uint64_t wstride;  // multiple of 16
+    uint32_t seq0, len;
+    uint32_t *wire_len;  // may be null
+    uint32_t cinit;
+    struct Pre {};
+    __device__ __forceinline__ void pre(uint64_t, Pre &) const {}
+    // buffer resource over the 4 wire slots of round packets p0 .. p0+3
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t round_rsrc(uint64_t p0) const {
+        return make_rsrc(wire + p0 * wstride, uint32_t(4 * wstride));
+    }
+    __device__ __forceinline__ void copy(__amdgpu_buffer_rsrc_t rs, uint32_t q, int32_t rel, bool valid,
+                                         u32x4 w) const {
+        const uint32_t o = valid ? q * uint32_t(wstride) + 16u + uint32_t(rel) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, int(o), 0, 2);  // aux 2: nt (streaming store)
+    }
+    __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
+        if (!on) return;
+        const u32x4 h = {bswap32(WTP_TYPE_DATA), bswap32(seq0 + uint32_t(p)), bswap32(len), bswap32(v ^ cinit)};
+        *reinterpret_cast<u32x4 *>(wire + p * wstride) = h;
+        if (wire_len) wire_len[p] = 16u + len;
     }
 };
 
@@ -310,11 +345,20 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
 
     auto crc_round = [&](uint64_t rr, const Round &R) {
         uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+        const auto crs = [&] {
+            if constexpr (BEpi::kCopy) return epi.round_rsrc(rr * 4);
+            else return 0;
+        }();
+        const bool qlive = rr * 4 + q < n;
 #pragma unroll
         for (int i = 0; i < ROWS; ++i) {
             u32x4 w = R.w[i];
+            const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(R.lead);
+            if constexpr (BEpi::kCopy) {
+                const bool in = (i == 0 || i == ROWS - 1) ? (rel >= 0 && rel < int32_t(len)) : true;
+                epi.copy(crs, q, rel, in && qlive, w);
+            }
             if (i == 0 || i == ROWS - 1) {
-                const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(R.lead);
                 if (!(rel >= 0 && rel < int32_t(len))) w = u32x4{0, 0, 0, 0};
             }
             if (DIAG & 1) {
@@ -785,9 +829,6 @@ struct DevState {
     uint32_t *tabs = nullptr;
     uint32_t *status = nullptr;
     int cus = 0;
-    std::mutex scratch_mu;
-    uint32_t *scratch = nullptr;
-    uint64_t scratch_words = 0;
 };
 constexpr int kMaxDev = 64;
 DevState g_dev[kMaxDev];
@@ -1159,40 +1200,56 @@ int wtp_build_data_packets(const void *d_payloads, size_t total_bytes, uint32_t 
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t nch = (total_bytes + WTP_MAX_PAYLOAD - 1) / WTP_MAX_PAYLOAD;
-    uint32_t *crc = d_wire_len;  // CRCs land here first, then become the lengths
-    if (!crc) {
-        std::lock_guard<std::mutex> g(s->scratch_mu);
-        if (s->scratch_words < nch) {
-            if (s->scratch) (void)hipFree(s->scratch);
-            s->scratch = nullptr;
-            s->scratch_words = 0;
-            WTP_HIP(hipMalloc(&s->scratch, nch * 4));
-            s->scratch_words = nch;
-        }
-        crc = s->scratch;
-    }
+    const uint64_t full = total_bytes / WTP_MAX_PAYLOAD;
+    const uint8_t *pay = static_cast<const uint8_t *>(d_payloads);
     uint8_t *wire = static_cast<uint8_t *>(d_wire);
+    // Fused path: the braided kernel reads each full chunk once, copies it into its wire
+    // slot and writes the header (16-B aligned buffers and slots).
+    const bool fused = reinterpret_cast<uintptr_t>(pay) % 16 == 0 && reinterpret_cast<uintptr_t>(wire) % 16 == 0 &&
+                       wire_stride % 16 == 0 && wire_stride <= 16384;
+    const uint64_t first = fused ? full : 0;  // chunks [first, nch) take the three-step path
+    if (fused && full &&
+        (rc = launch_fixed_braid(*s, pay, WTP_MAX_PAYLOAD, WTP_MAX_PAYLOAD, full,
+                                 dev::BuildBEpi{wire, wire_stride, seq0, WTP_MAX_PAYLOAD, d_wire_len, 0}, st)))
+        return rc;
+    const uint64_t nslow = nch - first;
+    if (!nslow) return WTP_OK;
+    // Three-step path (unaligned buffers, and the short last chunk): copy into the slots,
+    // CRC over the slots, then the headers.  CRCs land in d_wire_len first (then become
+    // the lengths), else in stream-ordered scratch.
+    const uint8_t *spay = pay + first * WTP_MAX_PAYLOAD;
+    uint8_t *swire = wire + first * wire_stride;
+    const uint64_t stotal = total_bytes - first * WTP_MAX_PAYLOAD;
+    uint32_t *crc = d_wire_len ? d_wire_len + first : nullptr;
+    uint32_t *tmp = nullptr;
+    if (!crc) {
+        WTP_HIP(hipMallocAsync(reinterpret_cast<void **>(&tmp), nslow * 4, st));
+        crc = tmp;
+    }
     {
-        const uint64_t work = nch * (WTP_MAX_PAYLOAD / 4 + 1);
+        const uint64_t work = nslow * (WTP_MAX_PAYLOAD / 4 + 1);
         uint64_t blocks = (work + 255) / 256;
         if (blocks > 65536) blocks = 65536;
-        hipLaunchKernelGGL(dev::k_wire_copy, dim3(unsigned(blocks)), dim3(256), 0, st,
-                           static_cast<const uint8_t *>(d_payloads), uint64_t(total_bytes), wire, uint64_t(wire_stride), nch);
-        if ((rc = launch_check("k_wire_copy"))) return rc;
+        hipLaunchKernelGGL(dev::k_wire_copy, dim3(unsigned(blocks)), dim3(256), 0, st, spay, stotal, swire,
+                           uint64_t(wire_stride), nslow);
+        rc = launch_check("k_wire_copy");
     }
-    // CRC over the payloads in their wire slots (full chunks take the braided path when
-    // the slot layout is 16-B aligned, e.g. wire_stride 1472).
-    const uint64_t full = total_bytes / WTP_MAX_PAYLOAD;
-    const uint64_t tail = total_bytes - full * WTP_MAX_PAYLOAD;
-    if (full && (rc = wtp_crc32_batch_fixed(wire + 16, wire_stride, WTP_MAX_PAYLOAD, full, crc, stream))) return rc;
-    if (tail && (rc = wtp_crc32_batch_fixed(wire + full * wire_stride + 16, 0, tail, 1, crc + full, stream))) return rc;
-    {
-        uint64_t blocks = (nch + 255) / 256;
+    const uint64_t sfull = stotal / WTP_MAX_PAYLOAD;
+    const uint64_t tail = stotal - sfull * WTP_MAX_PAYLOAD;
+    if (!rc && sfull) rc = wtp_crc32_batch_fixed(swire + 16, wire_stride, WTP_MAX_PAYLOAD, sfull, crc, stream);
+    if (!rc && tail) rc = wtp_crc32_batch_fixed(swire + sfull * wire_stride + 16, 0, tail, 1, crc + sfull, stream);
+    if (!rc) {
+        uint64_t blocks = (nslow + 255) / 256;
         if (blocks > 65536) blocks = 65536;
-        hipLaunchKernelGGL(dev::k_wire_header, dim3(unsigned(blocks)), dim3(256), 0, st, crc, uint64_t(total_bytes),
-                           seq0, wire, uint64_t(wire_stride), d_wire_len, nch);
-        if ((rc = launch_check("k_wire_header"))) return rc;
+        hipLaunchKernelGGL(dev::k_wire_header, dim3(unsigned(blocks)), dim3(256), 0, st, crc, stotal,
+                           seq0 + uint32_t(first), swire, uint64_t(wire_stride), crc == tmp ? nullptr : crc, nslow);
+        rc = launch_check("k_wire_header");
     }
+    if (tmp) {
+        const hipError_t fe = hipFreeAsync(tmp, st);
+        if (!rc && fe != hipSuccess) rc = fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
+    }
+    if (rc) return rc;
     return WTP_OK;
 }
 

@@ -346,6 +346,44 @@ def test_build_data_packets(W):
             assert w[i * 1472:i * 1472 + len(want)].tobytes() == want, (total, i)
 
 
+@pytest.mark.parametrize("total,stride,pay_off,wire_off,with_len,seq0", [
+    (1456 * 5000 + 333, 1472, 0, 0, True, 0),          # fused path + short tail
+    (1456 * 4099, 1472, 0, 0, False, 0xFFFFFFF0),      # fused, no tail, no lengths, seq wraps
+    (1456 * 777 + 1, 1488, 0, 0, True, 3),             # fused, wider 16-B slots
+    (1456 * 513 + 1000, 1500, 0, 0, True, 9),          # slot stride % 16 != 0: three-step path
+    (1456 * 300 + 17, 1472, 4, 0, True, 1),            # unaligned payloads: three-step path
+    (1456 * 300, 1472, 0, 8, False, 2),                # unaligned wire: three-step path
+])
+def test_build_data_packets_paths(W, total, stride, pay_off, wire_off, with_len, seq0):
+    host = O.synth_fill_np(total, start_byte=total + stride)
+    raw = np.zeros(total + pay_off + 16, np.uint8)
+    raw[pay_off:pay_off + total] = host
+    d = dev_u8(raw)[pay_off:]
+    nch = (total + 1455) // 1456
+    wraw = torch.full((nch * stride + wire_off,), 0xA5, dtype=torch.uint8, device="cuda")
+    wire = wraw[wire_off:]
+    wl = u32_out(nch) if with_len else None
+    W.build_data_packets(d, total, seq0, wire, stride, wl)
+    torch.cuda.synchronize()
+    w = wire.cpu().numpy()
+    lens = to_u32(wl, nch) if with_len else None
+    for i in list(range(min(nch, 40))) + list(range(max(40, nch - 40), nch)):
+        p = host[i * 1456:(i + 1) * 1456].tobytes()
+        want = O.build_datagram((seq0 + i) & 0xFFFFFFFF, p)
+        if with_len:
+            assert lens[i] == len(want)
+        got = w[i * stride:i * stride + len(want)].tobytes()
+        assert got == want, (i, got[:16].hex(), want[:16].hex())
+        assert (w[i * stride + len(want):(i + 1) * stride] == 0xA5).all()  # slot tail untouched
+    # every header's checksum vs an independent device CRC of the payload buffer
+    full = total // 1456
+    crcs = u32_out(full)
+    W.crc32_batch_fixed(d, 1456, 1456, full, crcs)
+    c = to_u32(crcs, full)
+    hdr = w[:full * stride].reshape(full, stride)[:, 12:16]
+    assert np.array_equal(hdr.copy().view(">u4").ravel(), c)
+
+
 def test_host_chunked_pageable_and_pinned(W):
     nbytes = 40 * (1 << 20) + 64  # crosses slab boundaries? (64 MiB slabs) keep moderate
     host = O.synth_fill_np(nbytes, start_byte=5)

@@ -173,3 +173,42 @@ def test_c1_gpu_verify_drops_corruption(binaries, tmp_path):
     out, slog, rlog, px = run_transfer(binaries, src, str(tmp_path), crc="gpu", proxy=True, timeout=120)
     assert open(out, "rb").read() == open(src, "rb").read()
     assert px.corrupted > 0
+
+
+def _recv_bench(bindir, crc, batch=256, seconds=1.0, corrupt=100):
+    import json
+    port = _free_port()
+    recv = subprocess.Popen([os.path.join(bindir, "wReceiver"), "--bench", str(seconds), "-p", str(port), "--crc", crc,
+                             "--batch", str(batch)], stdout=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.3)
+        s = subprocess.run([os.path.join(bindir, "wBlast"), "-h", "127.0.0.1", "-p", str(port), "--seconds",
+                            str(seconds), "--batch", "64", "--corrupt", str(corrupt)], capture_output=True, text=True,
+                           timeout=60)
+        assert s.returncode == 0, s.stderr
+        out, _ = recv.communicate(timeout=60)
+    finally:
+        if recv.poll() is None:
+            recv.kill()
+    return json.loads(s.stdout), json.loads(out)
+
+
+def test_batched_receive_bench_cpu(binaries):
+    """recvmmsg ring + batch verify.  Every 100th datagram carries a
+    flipped payload bit; exactly those must fail verify (up to UDP loss)."""
+    sent, got = _recv_bench(binaries, "cpu")
+    assert got["mode"] == "cpu" and got["datagrams"] > 1000
+    bad = got["datagrams"] - got["ok"]
+    assert 0.5 * got["datagrams"] / 100 <= bad <= 1.5 * got["datagrams"] / 100 + 2, got
+    assert sent["sent"] >= got["datagrams"]
+
+
+@pytest.mark.gpu
+def test_batched_receive_bench_gpu(binaries):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sent, got = _recv_bench(binaries, "gpu", batch=1024)
+    assert got["mode"] == "gpu" and got["datagrams"] > 1000
+    bad = got["datagrams"] - got["ok"]
+    assert 0.5 * got["datagrams"] / 100 <= bad <= 1.5 * got["datagrams"] / 100 + 2, got

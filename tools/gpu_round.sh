@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests -> bench -> rocprofv3 kernel-trace stats.
 # Every GPU step has its own time limit; a crash-type exit (fault, abort, segfault,
 # time limit) ends the script without starting further GPU work.
-#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg smoke
+#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg recv smoke
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -42,6 +42,17 @@ for s in $STEPS; do
            cd "$ROOT" ;;
     extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     cfg)   run cfg 600 python tools/bench_configs.py --only "${CFG_ONLY:-c5,verify}" --out "$OUT/configs.json" ;;
+    recv)  for m in cpu gpu; do for b in 64 1024; do
+             P=$((20000 + RANDOM % 20000))
+             timeout -k 10 60 ./a3-reliable-transport_amd/bin/wReceiver --bench 3 -p $P --crc $m --batch $b \
+               > "$OUT/recv_${m}_${b}.json" 2> "$OUT/recv_${m}_${b}.err" &
+             RP=$!; sleep 0.5
+             timeout -k 10 30 ./a3-reliable-transport_amd/bin/wBlast -h 127.0.0.1 -p $P --seconds 3 --batch 64 \
+               --corrupt 100 > "$OUT/blast_${m}_${b}.json" 2>&1
+             wait $RP; rc=$?
+             echo "recv $m $b rc=$rc: $(cat "$OUT/recv_${m}_${b}.json")" | tee -a "$OUT/steps.log"
+             if fatal "$rc"; then echo "FATAL rc=$rc in recv"; exit "$rc"; fi
+           done; done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done
