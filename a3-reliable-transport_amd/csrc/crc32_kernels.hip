@@ -79,6 +79,8 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // flags: the accesses are ds_* by construction, never flat.
 typedef __attribute__((address_space(3))) char lchar;
 typedef __attribute__((address_space(3))) u32x4 lu32x4;
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef __attribute__((address_space(3))) u32x4a4 lu32x4u;  // 4-B aligned LDS vector
 typedef __attribute__((address_space(3))) uint8_t lu8;
 
 __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
@@ -650,7 +652,6 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         const bool active = lane < total;
         const int32_t vf0 = int32_t(poff) - ws;  // bytes of the window before the packet
         const int32_t vf = active ? (vf0 > 64 ? 64 : vf0) : 64;
-        const uint32_t a = uint32_t(ws) & 15u;
 
         // --- stage the span ---------------------------------------------------------------
         const bool hit = __ballot(active && (ws < spec || we - spec > kSpanBytes)) == 0;
@@ -663,18 +664,29 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
         if (lane < kPcChunks - 256u) *(lu32x4 *)(slot + stage_addr(256u + lane)) = x[4];
-        __builtin_amdgcn_wave_barrier();
-        uint32_t d[20];
-        {
-            const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
+        // each 256-B group's padding gap repeats the next group's first chunk, so a
+        // 16-B read may run past the group end
 #pragma unroll
-            for (uint32_t u = 0; u < 5; ++u) {
-                const u32x4 y = *(const lu32x4 *)(slot + stage_addr(blk + u));
+        for (uint32_t i = 0; i < 5; ++i) {
+            const uint32_t c = 64u * i + lane;
+            if ((lane & 15u) == 0 && c != 0 && c < kPcChunks) *(lu32x4 *)(slot + 16u * (c + (c >> 4) - 1)) = x[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the window's 17 dwords from its 4-B aligned start (unaligned ds_read_b128)
+        uint32_t d[17];
+        {
+            const uint32_t x0 = active ? uint32_t(ws - sbase) & ~3u : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t l = x0 + 16u * u;
+                const u32x4 y = *(const lu32x4u *)(slot + l + 16u * (l >> 8));
                 d[4 * u + 0] = y.x;
                 d[4 * u + 1] = y.y;
                 d[4 * u + 2] = y.z;
                 d[4 * u + 3] = y.w;
             }
+            const uint32_t l = x0 + 64u;
+            d[16] = *(const __attribute__((address_space(3))) uint32_t *)(slot + l + 16u * (l >> 8));
         }
         __builtin_amdgcn_wave_barrier();
 
@@ -690,13 +702,9 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         spec = p0n < hi ? ((last_we - kPieceS) & ~15) : kNoSpan;
         load_span(rs, spec, lane, x);
 
-        // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
-        const uint32_t m2 = 0u - ((a >> 3) & 1u), m1 = 0u - ((a >> 2) & 1u), sb = a & 3u;
-        uint32_t e[18];
-#pragma unroll
-        for (int i = 0; i < 18; ++i) e[i] = d[i] ^ ((d[i] ^ d[i + 2]) & m2);
-#pragma unroll
-        for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
+        // byte funnel: word i = window bytes [4i, 4i + 4)
+        const uint32_t sb = uint32_t(ws) & 3u;
+        const uint32_t(&e)[17] = d;
 
         uint32_t c = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
         const int32_t vf8 = 8 * vf;

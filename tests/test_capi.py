@@ -63,7 +63,7 @@ def test_kernels_use_no_flat_memory_ops(tmp_path):
     if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
         pytest.skip("no ROCm llvm tools")
     dis = _gfx950_disassembly(W.LIB_PATH, tmp_path)
-    assert re.search(r"\bds_read_b128\b", dis) and re.search(r"\bbuffer_load_dwordx4\b", dis)
+    assert re.search(r"\bds_read_b32\b", dis) and re.search(r"\bbuffer_load_dwordx4\b", dis)
     flat = [l.strip() for l in dis.splitlines() if re.search(r"\bflat_\w+", l)]
     assert not flat, flat[:5]
 
