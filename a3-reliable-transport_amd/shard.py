@@ -16,16 +16,39 @@ def shard_range(rank: int, world: int, n: int) -> tuple[int, int]:
 
 
 def shard_byte_range(rank: int, world: int, n: int, stride: int) -> tuple[int, int]:
+    """Byte range of `rank`'s block of a fixed-stride batch."""
     lo, hi = shard_range(rank, world, n)
     return lo * stride, hi * stride
 
 
-def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None):
+def shard_by_bytes(rank: int, world: int, lengths) -> tuple[int, int]:
+    """Packets [lo, hi) of `rank` for a mixed-length batch, balanced by payload bytes
+    rather than by count: rank r starts at the first packet whose
+    exclusive byte prefix reaches r/world of the total.  Contiguous, disjoint, covering;
+    every rank's byte share is within one packet (<= 4096 B) of total/world."""
+    import numpy as np
+
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    lens = np.asarray(lengths, dtype=np.uint64)
+    excl = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]) if lens.size else np.zeros(0, np.uint64)
+    total = int(lens.sum()) if lens.size else 0
+
+    def start(r: int) -> int:
+        if r >= world:
+            return int(lens.size)
+        return int(np.searchsorted(excl, (total * r + world - 1) // world, side="left"))
+
+    return start(rank), start(rank + 1)
+
+
+def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None, out=None):
     """Gather every rank's int32 CRC tensor (equal lengths) to `dst`.
 
     Returns the concatenated tensor on `dst` (rank order = packet order for the block
-    partition) and None elsewhere.  With the "nccl" backend this is an RCCL gather over
-    xGMI; with "gloo" it runs on CPU tensors (tests).
+    partition) and None elsewhere.  `out` (on `dst`: world * local.numel() elements)
+    receives the result in place, with no allocation per call.  With the "nccl"
+    backend this is an RCCL gather over xGMI; with "gloo" it runs on CPU tensors.
     """
     import torch
     import torch.distributed as dist
@@ -33,8 +56,32 @@ def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None):
     if world == 1:
         return local
     if rank == dst:
-        parts = [torch.empty_like(local) for _ in range(world)]
+        full = out if out is not None else torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+        parts = list(full.view(world, -1).unbind(0))
         dist.gather(local, gather_list=parts, dst=dst, group=group)
-        return torch.cat(parts)
+        return full
     dist.gather(local, gather_list=None, dst=dst, group=group)
+    return None
+
+
+def gather_crcs_var(local, counts, rank: int, dst: int = 0, group=None):
+    """Gather per-rank CRC tensors of different lengths (the byte-balanced partition of
+    a mixed-length batch, shard_by_bytes) to `dst`.  `counts[r]` = rank r's packet
+    count, known to every rank (each computes the partition itself), so no extra
+    exchange is needed: every rank pads to max(counts), one gather moves the data, and
+    `dst` trims.  Returns the packet-ordered tensor on `dst`, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world = len(counts)
+    if world == 1:
+        return local
+    m = max(counts)
+    padded = torch.zeros(m, dtype=local.dtype, device=local.device)
+    padded[:local.numel()] = local
+    if rank == dst:
+        full = torch.empty(world * m, dtype=local.dtype, device=local.device)
+        dist.gather(padded, gather_list=list(full.view(world, m).unbind(0)), dst=dst, group=group)
+        return torch.cat([full[r * m:r * m + counts[r]] for r in range(world)])
+    dist.gather(padded, gather_list=None, dst=dst, group=group)
     return None

@@ -38,7 +38,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=30)  # past the DVFS transient of launches 2-20
     ap.add_argument("--packets-per-rank", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="target wall seconds of the 1-thread CPU-baseline leg (the all-thread leg runs 1/3 of it)")
@@ -138,11 +138,12 @@ def main():
     W.synth_fill(buf, start_byte=rank * nbytes, seed=SEED, nbytes=nbytes)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     do_gather = world > 1 and not args.no_gather
+    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
 
     def step():
         W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
         if do_gather:
-            shard.gather_crcs(out, world, rank)
+            shard.gather_crcs(out, world, rank, out=gathered)
 
     for _ in range(args.warmup):
         step()
@@ -159,7 +160,7 @@ def main():
         W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
         ends[i].record(stream)
         if do_gather:
-            shard.gather_crcs(out, world, rank)
+            shard.gather_crcs(out, world, rank, out=gathered)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -75,3 +75,65 @@ def test_gather_matches_single_process(world):
     import oracle as O
     want = O.batch_fixed(O.synth_fill_np(n_total * PAYLOAD), PAYLOAD, PAYLOAD, n_total)
     assert np.array_equal(got, want)
+
+
+def test_shard_by_bytes_balanced():
+    import oracle as O
+    for lens in (O.zipf_lengths(100_000, s=1.1), O.zipf_lengths(5000, s=1.0), np.full(7, 1456), np.array([4096] * 3),
+                 np.array([], dtype=np.uint32), np.array([0, 0, 5, 0])):
+        total = int(np.sum(lens, dtype=np.uint64))
+        for world in (1, 2, 3, 4, 8):
+            rs = [shard.shard_by_bytes(r, world, lens) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == len(lens)
+            for (a, b), (c, d) in zip(rs, rs[1:]):
+                assert b == c and a <= b
+            for a, b in rs:
+                share = int(np.sum(lens[a:b], dtype=np.uint64))
+                assert abs(share - total / world) <= 4096 + 1, (world, share, total / world)
+
+
+def _worker_var(rank, world, port, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd"), os.path.join(here, "..", "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    import shard as S
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lens = O.zipf_lengths(3000, s=1.1)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    data = O.synth_fill_np(int(lens.sum()), start_byte=77)
+    ranges = [S.shard_by_bytes(r, world, lens) for r in range(world)]
+    lo, hi = ranges[rank]
+    local = O.batch_var(data, offs[lo:hi], lens[lo:hi])
+    t = torch.from_numpy(local.view(np.int32).copy())
+    full = S.gather_crcs_var(t, [b - a for a, b in ranges], rank)
+    if rank == 0:
+        q.put(full.numpy().view(np.uint32).copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mixed_length_byte_shards_gather(world):
+    """C5-style batch: byte-balanced shards (unequal packet counts) + padded gather."""
+    import torch.multiprocessing as mp
+    import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_var, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    lens = O.zipf_lengths(3000, s=1.1)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    data = O.synth_fill_np(int(lens.sum()), start_byte=77)
+    assert np.array_equal(got, O.batch_var(data, offs, lens))
