@@ -79,8 +79,6 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // flags: the accesses are ds_* by construction, never flat.
 typedef __attribute__((address_space(3))) char lchar;
 typedef __attribute__((address_space(3))) u32x4 lu32x4;
-typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-typedef __attribute__((address_space(3))) u32x4a4 lu32x4u;  // 4-B aligned LDS vector
 typedef __attribute__((address_space(3))) uint8_t lu8;
 
 __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
@@ -664,29 +662,21 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
         if (lane < kPcChunks - 256u) *(lu32x4 *)(slot + stage_addr(256u + lane)) = x[4];
-        // each 256-B group's padding gap repeats the next group's first chunk, so a
-        // 16-B read may run past the group end
-#pragma unroll
-        for (uint32_t i = 0; i < 5; ++i) {
-            const uint32_t c = 64u * i + lane;
-            if ((lane & 15u) == 0 && c != 0 && c < kPcChunks) *(lu32x4 *)(slot + 16u * (c + (c >> 4) - 1)) = x[i];
-        }
         __builtin_amdgcn_wave_barrier();
-        // the window's 17 dwords from its 4-B aligned start (unaligned ds_read_b128)
-        uint32_t d[17];
+        // the window's five 16-B blocks, aligned (a dword-aligned variant without the
+        // rotation below was measured 13% slower on C5: its ds_read2_b32 pairs at a
+        // 64-B lane stride conflict 4-way)
+        uint32_t d[20];
         {
-            const uint32_t x0 = active ? uint32_t(ws - sbase) & ~3u : 0u;
+            const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const uint32_t l = x0 + 16u * u;
-                const u32x4 y = *(const lu32x4u *)(slot + l + 16u * (l >> 8));
+            for (uint32_t u = 0; u < 5; ++u) {
+                const u32x4 y = *(const lu32x4 *)(slot + stage_addr(blk + u));
                 d[4 * u + 0] = y.x;
                 d[4 * u + 1] = y.y;
                 d[4 * u + 2] = y.z;
                 d[4 * u + 3] = y.w;
             }
-            const uint32_t l = x0 + 64u;
-            d[16] = *(const __attribute__((address_space(3))) uint32_t *)(slot + l + 16u * (l >> 8));
         }
         __builtin_amdgcn_wave_barrier();
 
@@ -702,9 +692,14 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         spec = p0n < hi ? ((last_we - kPieceS) & ~15) : kNoSpan;
         load_span(rs, spec, lane, x);
 
-        // byte funnel: word i = window bytes [4i, 4i + 4)
-        const uint32_t sb = uint32_t(ws) & 3u;
-        const uint32_t(&e)[17] = d;
+        // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
+        const uint32_t a = uint32_t(ws) & 15u;
+        const uint32_t m2 = 0u - ((a >> 3) & 1u), m1 = 0u - ((a >> 2) & 1u), sb = a & 3u;
+        uint32_t e[18];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) e[i] = d[i] ^ ((d[i] ^ d[i + 2]) & m2);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
 
         uint32_t c = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
         const int32_t vf8 = 8 * vf;
@@ -730,8 +725,11 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
             const uint32_t u = __shfl_up(W, 1);
             if (lp >= 1u && lane >= 1u) W ^= stag_apply<128>(lds, K.kA, K.sel, u);
         }
+        // levels no lane needs (every packet of the round has < dd pieces in it) are
+        // skipped with a wave-uniform branch: small-packet rounds stop early
 #pragma unroll
         for (uint32_t dd = 2, o = 0; dd < 64; dd <<= 1, ++o) {
+            if (__ballot(lp >= dd && lane >= dd) == 0) break;
             const uint32_t u = __shfl_up(W, dd);
             if (lp >= dd && lane >= dd) W ^= op_apply(lds, kPcOps + o * kOpBytes, u);
         }
@@ -837,6 +835,7 @@ struct DevState {
     uint32_t *tabs = nullptr;
     uint32_t *status = nullptr;
     int cus = 0;
+    hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed
 };
 constexpr int kMaxDev = 64;
 DevState g_dev[kMaxDev];
@@ -878,6 +877,18 @@ int init_device(int dev) {
             return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
         if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
         if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
+        // Scratch of async entry points (verify fix-up list, builder CRCs) comes from a
+        // library-owned pool whose memory is kept across calls (release threshold max):
+        // the default threshold returns it at every synchronisation, and re-mapping it
+        // cost ~1 ms per small host-verify call.
+        hipMemPoolProps pp{};
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = dev;
+        if (hipMemPoolCreate(&s.pool, &pp) != hipSuccess) return setfail(WTP_EHIP, "hipMemPoolCreate failed");
+        uint64_t keep = UINT64_MAX;
+        if (hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
+            return setfail(WTP_EHIP, "hipMemPoolSetAttribute failed");
         (void)hipSetDevice(prev);
     });
     if (s.rc != WTP_OK) return fail(s.rc, "wtp init(device %d): %s", dev, s.err.c_str());
@@ -1154,7 +1165,7 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     if (stride % 16 == 0 && stride >= 32 && stride <= 1552 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
         const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
         uint32_t *fix = nullptr;
-        WTP_HIP(hipMallocAsync(reinterpret_cast<void **>(&fix), 4 * (std::min<uint64_t>(per, n) + 1), st));
+        WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&fix), 4 * (std::min<uint64_t>(per, n) + 1), s->pool, st));
         for (uint64_t p = 0; p < n && !rc; p += per) {
             const uint64_t cnt = std::min<uint64_t>(per, n - p);
             const uint8_t *sb = b + p * stride;
@@ -1231,7 +1242,7 @@ int wtp_build_data_packets(const void *d_payloads, size_t total_bytes, uint32_t 
     uint32_t *crc = d_wire_len ? d_wire_len + first : nullptr;
     uint32_t *tmp = nullptr;
     if (!crc) {
-        WTP_HIP(hipMallocAsync(reinterpret_cast<void **>(&tmp), nslow * 4, st));
+        WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&tmp), nslow * 4, s->pool, st));
         crc = tmp;
     }
     {

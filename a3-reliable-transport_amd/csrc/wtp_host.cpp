@@ -45,7 +45,8 @@ int hfail(int code, const char *what, hipError_t e) {
 
 struct Pipe {
     std::mutex mu;
-    bool ready = false;
+    std::once_flag once;
+    int rc = WTP_OK;
     hipStream_t st[2] = {nullptr, nullptr};
     uint8_t *pin_in[2] = {nullptr, nullptr};
     uint8_t *dev_in[2] = {nullptr, nullptr};
@@ -66,21 +67,25 @@ int pipe_get(Pipe *&out) {
     int rc = wtp_init(dev);
     if (rc) return rc;
     Pipe &p = g_pipe[dev];
-    if (!p.ready) {
-        p.max_pk = kSlabBytes / 16 + 1;  // worst case: 16-B datagrams / 1-B chunks capped below
-        for (int b = 0; b < 2; ++b) {
-            H_HIP(hipStreamCreateWithFlags(&p.st[b], hipStreamNonBlocking));
-            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_in[b]), kSlabBytes, hipHostMallocDefault));
-            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_in[b]), kSlabBytes + 64));
-            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_out[b]), p.max_pk * 4, hipHostMallocDefault));
-            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_out[b]), p.max_pk * 4));
-            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_aux[b]), p.max_pk * 4, hipHostMallocDefault));
-            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_aux[b]), p.max_pk * 4));
-            H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_ok[b]), p.max_pk, hipHostMallocDefault));
-            H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_ok[b]), p.max_pk));
-        }
-        p.ready = true;
-    }
+    std::call_once(p.once, [&p] {
+        auto mk = [&p]() -> int {
+            p.max_pk = kSlabBytes / 16 + 1;  // worst case: 16-B datagrams / 1-B chunks capped below
+            for (int b = 0; b < 2; ++b) {
+                H_HIP(hipStreamCreateWithFlags(&p.st[b], hipStreamNonBlocking));
+                H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_in[b]), kSlabBytes, hipHostMallocDefault));
+                H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_in[b]), kSlabBytes + 64));
+                H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_out[b]), p.max_pk * 4, hipHostMallocDefault));
+                H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_out[b]), p.max_pk * 4));
+                H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_aux[b]), p.max_pk * 4, hipHostMallocDefault));
+                H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_aux[b]), p.max_pk * 4));
+                H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_ok[b]), p.max_pk, hipHostMallocDefault));
+                H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_ok[b]), p.max_pk));
+            }
+            return WTP_OK;
+        };
+        p.rc = mk();
+    });
+    if (p.rc) return hfail(p.rc, "host pipeline setup failed", hipSuccess);
     out = &p;
     return WTP_OK;
 }
@@ -182,6 +187,8 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     if (rc) return rc;
     std::lock_guard<std::mutex> g(P->mu);
     const uint8_t *h = static_cast<const uint8_t *>(h_dgrams);
+    // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
+    const bool pinned = is_pinned(h_dgrams), lens_pinned = is_pinned(h_recv_len);
     const size_t per = std::min(P->max_pk, kSlabBytes / stride);
     Slab slot[2];
     size_t s = 0;
@@ -196,10 +203,18 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
         }
         if (first >= n) continue;
         const size_t cnt = std::min(per, n - first);
-        memcpy(P->pin_in[b], h + first * stride, cnt * stride);
-        memcpy(P->pin_aux[b], h_recv_len + first, cnt * 4);
-        H_HIP(hipMemcpyAsync(P->dev_in[b], P->pin_in[b], cnt * stride, hipMemcpyHostToDevice, P->st[b]));
-        H_HIP(hipMemcpyAsync(P->dev_aux[b], P->pin_aux[b], cnt * 4, hipMemcpyHostToDevice, P->st[b]));
+        const uint8_t *src = h + first * stride;
+        const uint32_t *lsrc = h_recv_len + first;
+        if (!pinned) {
+            memcpy(P->pin_in[b], src, cnt * stride);
+            src = P->pin_in[b];
+        }
+        if (!lens_pinned) {
+            memcpy(P->pin_aux[b], lsrc, cnt * 4);
+            lsrc = P->pin_aux[b];
+        }
+        H_HIP(hipMemcpyAsync(P->dev_in[b], src, cnt * stride, hipMemcpyHostToDevice, P->st[b]));
+        H_HIP(hipMemcpyAsync(P->dev_aux[b], lsrc, cnt * 4, hipMemcpyHostToDevice, P->st[b]));
         if ((rc = wtp_crc32_verify_batch(P->dev_in[b], stride, P->dev_aux[b], cnt, P->dev_ok[b], P->dev_out[b], P->st[b])))
             return rc;
         H_HIP(hipMemcpyAsync(P->pin_ok[b], P->dev_ok[b], cnt, hipMemcpyDeviceToHost, P->st[b]));

@@ -15,7 +15,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libwtp_crc32.so")
+# WTP_LIB selects another build of the same library (A/B kernel measurements); it must
+# exist like the default one does — there is no fallback.
+LIB_PATH = os.environ.get("WTP_LIB") or os.path.join(HERE, "lib", "libwtp_crc32.so")
 
 MAX_PAYLOAD = 1456
 MAX_KERNEL_LEN = 4096

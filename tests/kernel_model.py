@@ -196,9 +196,6 @@ def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
             a = stage_addr(c)
             assert a + 16 <= PC_SLOT
             slot[a:a + 16] = x[c]
-            if c % 16 == 0 and c:  # the previous group's gap repeats this chunk
-                g = 16 * (c + (c >> 4) - 1)
-                slot[g:g + 16] = x[c]
         # next round (prefetch)
         pk_l, lp_l, gp_l, _, _, K_l, _, we_l = act[-1]
         partial = gp_l + 1 < K_l
@@ -207,20 +204,11 @@ def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
         x = load_span(spec) if spec is not None else None
         vals = []
         for lane, (pk, lp, gp, off, L, K, ws, we) in enumerate(act):
-            # 17 dwords from the window's 4-B aligned start: 4 x 16-B reads (each may run
-            # into its group's gap copy) + 1 dword
-            x0 = (ws - sbase) & ~3
-            assert x0 >= 0
-            raw = b""
-            for u in range(4):
-                lo = x0 + 16 * u
-                ph = lo + 16 * (lo >> 8)
-                assert ph + 16 <= PC_SLOT
-                raw += bytes(slot[ph:ph + 16])
-            lo = x0 + 64
-            ph = lo + 16 * (lo >> 8)
-            raw += bytes(slot[ph:ph + 4])
-            window = bytearray(raw[ws & 3:(ws & 3) + S])
+            a = ws & 15
+            blk = (ws - sbase) >> 4
+            assert blk >= 0 and stage_addr(blk + 4) + 16 <= PC_SLOT
+            raw = b"".join(bytes(slot[stage_addr(blk + u):stage_addr(blk + u) + 16]) for u in range(5))
+            window = bytearray(raw[a:a + S])
             vf = min(off - ws, 64)
             for t in range(max(vf, 0)):
                 window[t] = 0

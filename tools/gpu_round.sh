@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests -> bench -> rocprofv3 kernel-trace stats.
 # Every GPU step has its own time limit; a crash-type exit (fault, abort, segfault,
 # time limit) ends the script without starting further GPU work.
-#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg recv smoke
+#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg profcfg ab recv smoke
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -40,6 +40,9 @@ for s in $STEPS; do
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
              -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
            cd "$ROOT" ;;
+    profcfg) cd /tmp && run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/profcfg" -o cfg -- python3 "$ROOT/tools/bench_configs.py" --only c2,c5,verify --out "$OUT/profcfg_configs.json"
+           cd "$ROOT" ;;
     extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     cfg)   run cfg 600 python tools/bench_configs.py --only "${CFG_ONLY:-c5,verify}" --out "$OUT/configs.json" ;;
     recv)  for m in cpu gpu; do for b in 64 1024; do
@@ -53,6 +56,10 @@ for s in $STEPS; do
              echo "recv $m $b rc=$rc: $(cat "$OUT/recv_${m}_${b}.json")" | tee -a "$OUT/steps.log"
              if fatal "$rc"; then echo "FATAL rc=$rc in recv"; exit "$rc"; fi
            done; done ;;
+    ab)    for lib in a3-reliable-transport_amd/lib/ab/*.so; do
+             v=$(basename "$lib" .so)
+             WTP_LIB="$ROOT/$lib" run "ab_$v" 300 python tools/bench_configs.py --only "${CFG_ONLY:-c5}" --out "$OUT/ab_$v.json"
+           done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done
