@@ -318,7 +318,14 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
                 const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(lead);
                 o = (rel >= 0 && rel < int32_t(len)) ? o : po;
             }
-            R.w[i] = __builtin_nontemporal_load((gu32x4 *)(sb + o));
+            // Row 0 holds the cache line a packet shares with the previous one: a normal
+            // load keeps it in L2 for that packet's last row; every other row streams
+            // (nt).  All-nt re-fetched the shared lines (HBM traffic 1.069x algorithmic)
+            // and was 4.7% slower; all-plain loads were 8.7% slower (A/B, same box).
+            if (i == 0)
+                R.w[i] = *(gu32x4 *)(sb + o);
+            else
+                R.w[i] = __builtin_nontemporal_load((gu32x4 *)(sb + o));
         }
     };
 

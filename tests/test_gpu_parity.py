@@ -328,6 +328,25 @@ def test_host_verify(W):
     assert np.array_equal(ok, want_ok) and np.array_equal(crc, want_crc)
 
 
+def test_host_verify_pinned_ring(W):
+    """wReceiver's path: a pinned (wtp_host_alloc) 1472-B ring is copied to the device
+    directly and verified by the braided kernel + fix-up; the recv_len array is pinned
+    too.  Includes runts, short, oversize and corrupted datagrams."""
+    rng = np.random.default_rng(21)
+    n, stride = 2500, 1472
+    buf, rl = _full_ring(n, stride, rng, 0.85)
+    ring = W.PinnedBuffer(n * stride)
+    ring.array[:] = buf
+    lens = W.PinnedBuffer(n * 4)
+    la = lens.array.view(np.uint32)
+    la[:] = rl
+    ok, crc = W.host_verify(ring.array, stride, la)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    assert np.array_equal(ok, want_ok) and np.array_equal(crc, want_crc)
+    ring.free()
+    lens.free()
+
+
 def test_build_data_packets(W):
     for total in (64, 1456, 2216, 10202, 1456 * 300 + 17):
         host = O.synth_fill_np(total, start_byte=total)
