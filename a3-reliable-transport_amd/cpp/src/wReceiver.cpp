@@ -21,12 +21,15 @@
 // ring of --batch slots (default: the window size), the whole batch is verified with one
 // call (one GPU launch with --crc gpu), then processed in arrival order exactly as
 // one-at-a-time reception would.  --bench measures that path alone: it receives DATA
-// datagrams (e.g. from wBlast) for the given seconds and prints one JSON line with the
-// receive+verify rate.
+// datagrams (e.g. from wBlast) for the given seconds, verifying each batch on a worker
+// thread while the next one arrives, and prints one JSON line with the rate.
 #include <time.h>
 
+#include <condition_variable>
 #include <fstream>
 #include <iostream>
+#include <mutex>
+#include <thread>
 
 #include "common/Endpoint.hpp"
 
@@ -49,37 +52,82 @@ double now_s() {
 
 // Receive + verify throughput (no protocol): prints
 // {"datagrams":..,"payload_bytes":..,"seconds":..,"GBps":..,"ok":..,"batches":..,...}
+// Two rings alternate: a worker thread verifies batch k (one GPU call with --crc gpu)
+// while the main thread receives batch k+1 into the other ring.
 int bench(int fd, const Checksums &crc, size_t batch, double seconds) {
     int big = 64 << 20;
     setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
     set_rcv_timeout_ms(fd, 500);
-    RecvRing ring(batch, crc.gpu());
+    RecvRing ring0(batch, crc.gpu()), ring1(batch, crc.gpu());
+    RecvRing *rings[2] = {&ring0, &ring1};
     uint64_t dgrams = 0, bytes = 0, good = 0, batches = 0;
     double t0 = 0, t1 = 0, tverify = 0;
-    for (;;) {
-        const size_t got = ring.receive(fd);
+
+    std::mutex mu;
+    std::condition_variable cv;
+    RecvRing *job = nullptr;  // batch handed to the worker
+    size_t job_n = 0;
+    bool busy = false, stop = false;
+    std::thread worker([&] {
+        for (;;) {
+            RecvRing *r;
+            size_t n;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return job != nullptr || stop; });
+                if (!job) return;
+                r = job;
+                n = job_n;
+            }
+            const double tv = now_s();
+            crc.verify_batch(r->ring(), RecvRing::kSlot, r->lens(), n, r->ok());
+            const double dv = now_s() - tv;
+            uint64_t b = 0, g = 0;
+            for (size_t i = 0; i < n; ++i) {
+                b += r->len(i) > kHeaderBytes ? r->len(i) - kHeaderBytes : 0;
+                g += r->ok()[i];
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            tverify += dv;
+            dgrams += n;
+            bytes += b;
+            good += g;
+            ++batches;
+            job = nullptr;
+            busy = false;
+            cv.notify_all();
+        }
+    });
+    for (int k = 0;; k ^= 1) {
+        const size_t got = rings[k]->receive(fd);  // the other ring may be under verify
         const double t = now_s();
-        if (!got) {
-            if (t0 > 0) break;  // the sender stopped
-            continue;
+        if (got && t0 == 0) t0 = t;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return !busy; });
+            if (got) {
+                job = rings[k];
+                job_n = got;
+                busy = true;
+                cv.notify_all();
+            }
         }
-        if (t0 == 0) t0 = t;
-        const double tv = now_s();
-        crc.verify_batch(ring.ring(), RecvRing::kSlot, ring.lens(), got, ring.ok());
-        tverify += now_s() - tv;
-        for (size_t i = 0; i < got; ++i) {
-            ++dgrams;
-            bytes += ring.len(i) > kHeaderBytes ? ring.len(i) - kHeaderBytes : 0;
-            good += ring.ok()[i];
-        }
-        ++batches;
+        if (!got && t0 > 0) break;  // the sender stopped
         t1 = now_s();
-        if (t1 - t0 >= seconds) break;
+        if (t0 > 0 && t1 - t0 >= seconds) break;
     }
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !busy; });
+        stop = true;
+        cv.notify_all();
+    }
+    worker.join();
+    t1 = now_s();
     const double dt = t1 > t0 ? t1 - t0 : 1e-9;
     std::printf("{\"mode\": \"%s\", \"batch_slots\": %zu, \"datagrams\": %llu, \"payload_bytes\": %llu, "
                 "\"seconds\": %.4f, \"GBps\": %.4f, \"datagrams_per_s\": %.0f, \"ok\": %llu, \"batches\": %llu, "
-                "\"verify_seconds\": %.4f, \"verify_GBps\": %.3f}\n",
+                "\"verify_seconds\": %.4f, \"verify_GBps\": %.3f, \"overlapped\": true}\n",
                 crc.gpu() ? "gpu" : "cpu", batch, (unsigned long long)dgrams, (unsigned long long)bytes, dt,
                 double(bytes) / dt / 1e9, double(dgrams) / dt, (unsigned long long)good, (unsigned long long)batches,
                 tverify, tverify > 0 ? double(bytes) / tverify / 1e9 : 0.0);
