@@ -65,6 +65,8 @@ constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 wo
 // conflict-free), then x^-256, x^-512, x^-1024 as plain 4 KiB operators.
 constexpr uint32_t kBraidPlainOps = 131072;
 constexpr uint32_t kBraidLdsWords = (kBraidPlainOps + 3 * kOpBytes) / 4;  // 143,360 B
+constexpr uint32_t kBraidXpose = 131072;                                 // Horner variant
+constexpr uint32_t kBraidHornerLdsWords = (kBraidXpose + 16 * 2048) / 4;  // 163,840 B
 
 namespace dev {
 
@@ -152,6 +154,10 @@ __device__ __forceinline__ void fill_stag(char *lds, uint32_t region, uint32_t s
 // after it are undone at the end with x^(-8T) (T/16 < 16: inverse ops 16..128 B).
 constexpr int kBraidFrame = 1;
 constexpr int kBraidDepth = 1;  // rounds of loads kept in flight beyond the one in use
+// VAR bit0: the first and last frame rows load through a per-round buffer resource with an
+// out-of-range offset for lanes outside the packet (no request, reads 0: no clamp, no
+// zeroing); bit1: the next row's data word is folded into the lookup XOR (xor3 of xor3).
+constexpr int kBraidVar = 7;
 
 // Bytes of frame before the packet start (st = packet address, 16-B aligned).
 __device__ __forceinline__ uint32_t braid_lead(uintptr_t st, uint32_t len, uint32_t frame) {
@@ -179,6 +185,16 @@ __device__ __forceinline__ uint32_t braid_lead(uintptr_t st, uint32_t len, uint3
 // one instruction.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t stag_apply3x(const char *lds, const uint32_t (&key)[4], const uint32_t (&sel)[4],
+                                                 uint32_t x, uint32_t w) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, key[0], sel[0]);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, key[1], sel[1]);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, key[2], sel[2]);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, key[3], sel[3]);
+    return xor3(xor3(lds_rd(lds, a0 + OFF), lds_rd(lds, a1 + OFF), lds_rd(lds, a2 + OFF)), lds_rd(lds, a3 + OFF), w);
 }
 
 template <uint32_t OFF>
@@ -274,11 +290,16 @@ struct BuildBEpi {
     }
 };
 
-template <int ROWS, int FRAME = kBraidFrame, int DIAG = 0, int DEPTH = kBraidDepth, class BEpi = CrcBEpi>
+template <int ROWS, int FRAME = kBraidFrame, int DIAG = 0, int DEPTH = kBraidDepth, class BEpi = CrcBEpi,
+          int VAR = kBraidVar>
 __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
                                                       const uint32_t *__restrict__ gtab) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];
+    // VAR bit2 (Horner combine): region B = {x^-128, x^-1024}, no plain operators, and a
+    // 2 KiB transposition slot per wave after the two regions (160 KiB in all).
+    constexpr bool kHorner = (VAR & 4) != 0;
+    constexpr uint32_t kFlushRounds = kHorner ? 8u : 16u;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kHorner ? kBraidHornerLdsWords : kBraidLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -311,9 +332,19 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             FRAME ? braid_lead(uint32_t(reinterpret_cast<uintptr_t>((const void *)sb)) + po, len, kFrame) : kFrame - len;
         R.lead = lead;
         const uint32_t fo = po - lead + j * 16u;  // frame column offset (used by rows >= 1)
+        [[maybe_unused]] const __amdgpu_buffer_rsrc_t rs = make_rsrc((const void *)sb, 3u * stride + len);  // every in-packet byte of the round (stride may be 0)
 #pragma unroll
         for (int i = 0; i < ROWS; ++i) {
             uint32_t o = fo + uint32_t(i) * 256u;
+            if ((VAR & 1) && (i == 0 || i == ROWS - 1)) {
+                const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(lead);
+                o = (rel >= 0 && rel < int32_t(len)) ? o : 0x80000000u;
+                if (i == 0)
+                    R.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(o), 0, 0));
+                else
+                    R.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(o), 0, 2));
+                continue;
+            }
             if (i == 0 || i == ROWS - 1) {  // may hold frame bytes outside the packet
                 const int32_t rel = int32_t(uint32_t(i) * 256u + j * 16u) - int32_t(lead);
                 o = (rel >= 0 && rel < int32_t(len)) ? o : po;
@@ -334,7 +365,49 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     uint64_t rfirst = 0;         // round of slot group 0
     typename BEpi::Pre pre{};    // epilogue loads for the current group
     // packet of lane 4k + q in the group starting at round g0
-    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 2) * rstep) * 4 + (lane & 3u); };
+    // (Horner: lane 2P + h, P = 4k + q, holds half h of packet slot q of round k)
+    auto group_packet = [&](uint64_t g0) {
+        if constexpr (kHorner) return (g0 + uint64_t(lane >> 3) * rstep) * 4 + ((lane >> 1) & 3u);
+        else return (g0 + uint64_t(lane >> 2) * rstep) * 4 + (lane & 3u);
+    };
+
+    // Horner flush: every round wrote its 64 column values v(k, q, j) to the wave's slot
+    // at [k][q][j]; lane 2P + h reads columns 8h .. 8h+7 of packet P and evaluates
+    // XOR_j x^(-128 j) v_j by Horner's rule (7 applies), the h = 1 half is moved by
+    // x^-1024, both halves take the trailing-zero fix x^(-128 t), and the pair is XORed.
+    auto flush_horner = [&](uint64_t next_g0, bool more) {
+        const lchar *xs = (const lchar *)(lds + kBraidXpose + wave * 2048u);
+        __builtin_amdgcn_wave_barrier();
+        const u32x4 lo = *(const lu32x4 *)(xs + lane * 32u), hi = *(const lu32x4 *)(xs + lane * 32u + 16u);
+        uint32_t acc = hi.w;
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.z);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.y);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.x);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.w);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.z);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.y);
+        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.x);
+        const uint32_t h = lane & 1u;
+        {
+            const uint32_t y = stag_apply3<128>(lds, K.kB, K.sel, acc);  // x^-1024
+            acc = h ? y : acc;
+        }
+        const uint64_t rr = rfirst + uint64_t(lane >> 3) * rstep;
+        const uint64_t p = rr * 4 + ((lane >> 1) & 3u);
+        if constexpr (FRAME != 0) {
+            const uint32_t st = uint32_t(reinterpret_cast<uintptr_t>(base)) + uint32_t(p) * stride;
+            const uint32_t t = (kFrame - len - braid_lead(st, len, kFrame)) >> 4;
+            const uint32_t tmax = (kFrame - len) >> 4;  // wave-uniform
+            for (uint32_t s = 0; s < tmax; ++s) {
+                const uint32_t y = stag_apply3<0>(lds, K.kB, K.sel, acc);  // x^-128
+                acc = s < t ? y : acc;
+            }
+        }
+        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(acc), 0xB1, 0xF, 0xF, false));  // lane ^ 1
+        epi.put(p, acc, h == 0 && (lane >> 3) < k && rr < rounds && p < n, pre);
+        if (more) epi.pre(group_packet(next_g0), pre);
+        k = 0;
+    };
 
     auto flush = [&](uint64_t next_g0, bool more) {
         const uint32_t t = colt >> 4;  // x^(-8T), T = 16t
@@ -365,7 +438,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
                 const bool in = (i == 0 || i == ROWS - 1) ? (rel >= 0 && rel < int32_t(len)) : true;
                 epi.copy(crs, q, rel, in && qlive, w);
             }
-            if (i == 0 || i == ROWS - 1) {
+            if (!(VAR & 1) && (i == 0 || i == ROWS - 1)) {
                 if (!(rel >= 0 && rel < int32_t(len))) w = u32x4{0, 0, 0, 0};
             }
             if (DIAG & 1) {
@@ -373,6 +446,23 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
                 b1 = (b1 ^ w.y) + (b1 >> 3);
                 b2 = (b2 ^ w.z) + (b2 >> 3);
                 b3 = (b3 ^ w.w) + (b3 >> 3);
+                continue;
+            }
+            if (VAR & 2) {  // b holds B ^ w of the current row; the last row applies plain
+                if (i == 0) {
+                    b0 = w.x; b1 = w.y; b2 = w.z; b3 = w.w;
+                } else {
+                    b0 = stag_apply3x<0>(lds, K.kA, K.sel, b0, w.x);
+                    b1 = stag_apply3x<0>(lds, K.kA, K.sel, b1, w.y);
+                    b2 = stag_apply3x<0>(lds, K.kA, K.sel, b2, w.z);
+                    b3 = stag_apply3x<0>(lds, K.kA, K.sel, b3, w.w);
+                }
+                if (i == ROWS - 1) {
+                    b0 = stag_apply3<0>(lds, K.kA, K.sel, b0);
+                    b1 = stag_apply3<0>(lds, K.kA, K.sel, b1);
+                    b2 = stag_apply3<0>(lds, K.kA, K.sel, b2);
+                    b3 = stag_apply3<0>(lds, K.kA, K.sel, b3);
+                }
                 continue;
             }
             b0 = stag_apply3<0>(lds, K.kA, K.sel, b0 ^ w.x);
@@ -383,6 +473,19 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
         // braid b = 4j + k holds R_0(frame_b) * x^(32 b): fold with x^(-32 k) (dense,
         // conflict-free staggered operators), then across lanes with x^(-128 j).
         uint32_t v;
+        if constexpr (kHorner) {
+            if (DIAG & 2) {
+                v = xor3(b0, b1, b2) ^ b3;
+            } else {  // b0 ^ x^-32 (b1 ^ x^-32 (b2 ^ x^-32 b3))
+                v = stag_apply3x<128>(lds, K.kA, K.sel, b3, b2);
+                v = stag_apply3x<128>(lds, K.kA, K.sel, v, b1);
+                v = stag_apply3x<128>(lds, K.kA, K.sel, v, b0);
+            }
+            if (k == 0) rfirst = rr;
+            *(__attribute__((address_space(3))) uint32_t *)(lds + kBraidXpose + wave * 2048u + k * 256u + lane * 4u) = v;
+            if (++k == kFlushRounds) flush_horner(rr + rstep, true);
+            return;
+        }
         if (DIAG & 2) {
             v = xor3(b0, b1, b2) ^ b3;
         } else {
@@ -417,9 +520,12 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     if (DEPTH == 2) load_round(r + rstep, B);
     fill_stag(lds, 0, 0, gtab + OFF_BRAID);
     fill_stag(lds, 0, 1, gtab + OFF_INV + 0 * 1024);  // x^-32
-    fill_stag(lds, 1, 0, gtab + OFF_INV + 1 * 1024);  // x^-64
-    fill_stag(lds, 1, 1, gtab + OFF_INV + 2 * 1024);  // x^-128
-    {
+    if constexpr (kHorner) {
+        fill_stag(lds, 1, 0, gtab + OFF_INV + 2 * 1024);  // x^-128
+        fill_stag(lds, 1, 1, gtab + OFF_INV + 5 * 1024);  // x^-1024
+    } else {
+        fill_stag(lds, 1, 0, gtab + OFF_INV + 1 * 1024);  // x^-64
+        fill_stag(lds, 1, 1, gtab + OFF_INV + 2 * 1024);  // x^-128
         u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kBraidPlainOps);
         const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_INV + 3 * 1024);
         for (uint32_t i = threadIdx.x; i < 3 * 256; i += blockDim.x) dst[i] = src[i];
@@ -451,7 +557,10 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             r += rstep;
         }
     }
-    if (k) flush(0, false);
+    if (k) {
+        if constexpr (kHorner) flush_horner(0, false);
+        else flush(0, false);
+    }
 }
 
 // ------------------------------------------------------------------------------------

@@ -38,7 +38,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=30)  # past the DVFS transient of launches 2-20
+    ap.add_argument("--warmup", type=int, default=100)  # past the DVFS transient of launches ~2-80
     ap.add_argument("--packets-per-rank", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="target wall seconds of the 1-thread CPU-baseline leg (the all-thread leg runs 1/3 of it)")

@@ -15,6 +15,7 @@
 #include <functional>
 #include <cstring>
 #include <unistd.h>
+#include <string>
 
 using namespace wtp;
 using namespace wtp::dev;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(1024) void k_g64_probe(const uint8_t *__restrict__ 
             w[dd][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + 1024 + lane * 16u));
         }
 #pragma unroll
-        for (int dd = 0; dd < DEPTH; ++dd) acc ^= w[dd][0].x ^ w[dd][0].w ^ w[dd][1].y ^ w[dd][1].z;
+        for (int dd = 0; dd < DEPTH; ++dd) acc ^= w[dd][0].x ^ w[dd][0].y ^ w[dd][0].z ^ w[dd][0].w ^ w[dd][1].x ^ w[dd][1].y ^ w[dd][1].z ^ w[dd][1].w;
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -300,6 +301,10 @@ int main(int argc, char **argv) {
     vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+#define BV(NAME, FR, VAR, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, FR, DIAG, 1, CrcBEpi, VAR>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
+    BV("var1_oob", 1, 1, 0); BV("var2_xor", 1, 2, 0); BV("var3_both", 1, 3, 0); BV("var0_skel", 1, 0, 3); BV("var1_skel", 1, 1, 3);
+    BV("var4_horner", 1, 4, 0); BV("var6_horner_xor", 1, 6, 0); BV("var7_all", 1, 7, 0); BV("var7_f0", 0, 7, 0);
+    BV("var6_f0", 0, 6, 0); BV("var7_nolut", 1, 7, 1); BV("var7_nocomb", 1, 7, 2); BV("var7_skel", 1, 7, 3); BV("var7_f0_skel", 0, 7, 3);
     vs.push_back({"new_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
     vs.push_back({"new_nocomb_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
     vs.push_back({"new_nolut", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
@@ -332,6 +337,13 @@ int main(int argc, char **argv) {
     vs.push_back({"pieces_fixed", [&] {  // general kernel, fixed provider
         launch_pieces(s, buf, bytes, dev::FixedProvL{1456, 0, 1456u}, n, dev::CrcEpi{out, uint32_t(n)}, nullptr); }, {}});
 
+    if (const char *only = getenv("KB_ONLY")) {  // comma-separated exact names; braid_prod always kept first
+        std::vector<V> keep;
+        std::string o = std::string(",") + only + ",";
+        for (auto &v : vs)
+            if (!strcmp(v.name, "braid_prod") || o.find(std::string(",") + v.name + ",") != std::string::npos) keep.push_back(v);
+        vs.swap(keep);
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     for (auto &v : vs) { v.f(); v.f(); }
@@ -370,11 +382,13 @@ int main(int argc, char **argv) {
     }
     // back-to-back launches of the production kernel (as bench.py issues them)
     {
+        size_t bp = 0;
+        for (size_t k = 0; k < vs.size(); ++k) if (!strcmp(vs[k].name, "braid_prod")) bp = k;
         std::vector<hipEvent_t> ev(2 * reps);
         for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
         for (int r = 0; r < reps; ++r) {
             CK(hipEventRecord(ev[2 * r], 0));
-            vs[3].f();
+            vs[bp].f();
             CK(hipEventRecord(ev[2 * r + 1], 0));
         }
         CK(hipDeviceSynchronize());
@@ -383,6 +397,21 @@ int main(int argc, char **argv) {
         std::sort(t.begin(), t.end());
         printf("braid_prod back-to-back: median %.4f ms (%.1f GB/s) min %.4f max %.4f\n", t[t.size() / 2],
                bytes / (t[t.size() / 2] * 1e-3) / 1e9, t[0], t.back());
+    }
+    {  // correctness of the var* variants against braid_prod (same outputs, bit-exact)
+        std::vector<uint32_t> ref(n), got(n);
+        size_t bp = 0;
+        for (size_t k = 0; k < vs.size(); ++k) if (!strcmp(vs[k].name, "braid_prod")) bp = k;
+        CK(hipMemset(out, 0, n * 4)); vs[bp].f(); CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ref.data(), out, n * 4, hipMemcpyDeviceToHost));
+        for (auto &v : vs) {
+            if (strncmp(v.name, "var", 3) || strstr(v.name, "skel")) continue;
+            CK(hipMemset(out, 0, n * 4)); v.f(); CK(hipDeviceSynchronize());
+            CK(hipMemcpy(got.data(), out, n * 4, hipMemcpyDeviceToHost));
+            uint64_t bad = 0;
+            for (uint64_t i = 0; i < n; ++i) bad += ref[i] != got[i];
+            printf("CHECK %-20s %s (%llu mismatches)\n", v.name, bad ? "MISMATCH" : "ok", (unsigned long long)bad);
+        }
     }
     printf("# n=%llu packets x 1456 B = %.3f GB per launch, grid(braid)=%u, reps=%d\n", (unsigned long long)n, bytes / 1e9, grid, reps);
     for (auto &v : vs) {
