@@ -2,12 +2,15 @@
 // Builds against the product kernel source and times, in one process with interleaved
 // rounds (guide §5.4 rule 24):
 //   read_probe   : the HBM read ceiling of this access shape (dwordx4 nt loads + XOR)
-//   braid        : the production k_fixed_braid<6>
-//   braid_nolut  : same loads/loop, table lookups replaced by XOR (memory + VALU only)
-//   braid_nocomb : production lookups, the x^-k folds and cross-lane tree removed
-// Output: one line per variant with median/min time and GB/s on 1M x 1456 B.
+//   braid_prod   : the production k_fixed_braid<6>
+//   braid_nolut  : same loads/loop, table lookups replaced by XOR/shift (DIAG 1)
+//   braid_nofold : production lookups, the in-lane x^-32 fold removed (DIAG 2)
+//   braid_skel   : both (DIAG 3): the loop skeleton's loads, flush and stores
+//   *_probe      : load-only access shapes (no compute)
+// KB_ONLY=a,b,c selects variants, KB_SUSTAIN=... times them back to back (KB_NS launches,
+// KB_REPS interleaved rounds).  Variants named var* are checked bit-exact against
+// braid_prod.  Output: one line per variant with median/min time and GB/s on 1M x 1456 B.
 #include "../a3-reliable-transport_amd/csrc/crc32_kernels.hip"
-#include "kbench_legacy.hpp"
 
 #include <algorithm>
 #include <cstdio>
@@ -27,71 +30,6 @@ __global__ __launch_bounds__(1024) void k_read_probe(const u32x4 *__restrict__ p
         acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
     if (acc == 0x12345678u) out[0] = acc;
-}
-
-// MODE bit0: no table lookups; bit1: no combine
-template <int ROWS, int MODE>
-__global__ __launch_bounds__(1024) void k_braid_diag(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
-                                                     uint64_t n, uint32_t *__restrict__ out,
-                                                     const uint32_t *__restrict__ gtab, uint32_t cinit) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLdsWords];
-    char *lds = reinterpret_cast<char *>(lds_w);
-    fill_replicated(lds, gtab + OFF_BRAID);
-    fill_ops(lds, gtab + OFF_INV, 6);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
-    const uint32_t j = lane & (kG - 1), q = lane >> 4;
-    const RepKeys K(lane);
-    constexpr uint32_t kFrame = 256u * ROWS;
-    const uint32_t zc = (kFrame - len) >> 4;
-    const uint64_t rounds = (n + 3) >> 2;
-    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
-    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
-    auto load_round = [&](uint64_t rr, u32x4 (&w)[ROWS]) {
-        uint64_t p = rr * 4 + q;
-        p = p < n ? p : n - 1;
-        const uint8_t *fs = base + p * stride + len - kFrame;
-#pragma unroll
-        for (int i = 0; i < ROWS; ++i) {
-            const uint32_t c = uint32_t(i) * kG + j;
-            if (c >= zc) w[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fs + c * 16u));
-            else w[i] = u32x4{0, 0, 0, 0};
-        }
-    };
-    u32x4 nxt[ROWS];
-    if (r < rounds) load_round(r, nxt);
-    for (; r < rounds; r += rstep) {
-        u32x4 w[ROWS];
-#pragma unroll
-        for (int i = 0; i < ROWS; ++i) w[i] = nxt[i];
-        if (r + rstep < rounds) load_round(r + rstep, nxt);
-        uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-#pragma unroll
-        for (int i = 0; i < ROWS; ++i) {
-            if (MODE & 1) {
-                b0 = (b0 ^ w[i].x) * 3u; b1 = (b1 ^ w[i].y) * 3u; b2 = (b2 ^ w[i].z) * 3u; b3 = (b3 ^ w[i].w) * 3u;
-            } else {
-                b0 = rep_word(lds, K, b0 ^ w[i].x);
-                b1 = rep_word(lds, K, b1 ^ w[i].y);
-                b2 = rep_word(lds, K, b2 ^ w[i].z);
-                b3 = rep_word(lds, K, b3 ^ w[i].w);
-            }
-        }
-        uint32_t v;
-        if (MODE & 2) {
-            v = b0 ^ b1 ^ b2 ^ b3;
-        } else {
-            v = b0 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b1) ^
-                op_apply(lds, kRepBytes + 1 * kOpBytes, b2 ^ op_apply(lds, kRepBytes + 0 * kOpBytes, b3));
-#pragma unroll
-            for (uint32_t d = 1, o = 2; d < kG; d <<= 1, ++o) {
-                const uint32_t u = __shfl_down(v, d, kG);
-                if ((j & (2 * d - 1)) == 0) v ^= op_apply(lds, kRepBytes + o * kOpBytes, u);
-            }
-        }
-        const uint64_t p = r * 4 + q;
-        if (j == 0 && p < n) out[p] = v ^ cinit;
-    }
 }
 
 // Same load pattern as the braid (16 lanes x 16 B per packet row, 4 packets/wave),
@@ -154,18 +92,9 @@ __global__ __launch_bounds__(1024) void k_g64_probe(const uint8_t *__restrict__ 
 // Generic braid-shaped load probe: G lanes x 16 B per packet row, 64/G packets per wave,
 // ROWS rows, DEPTH rounds in flight.  AL=0: frame right-aligned to the packet end (as the
 // production kernel); AL=1: frame start 128-B aligned when it fits, else 64-B aligned.
-template <int G, int ROWS, int AL, int DEPTH, int LDSF = 0>
-__global__ __launch_bounds__(1024) void k_gprobe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out,
-                                                 const uint32_t *__restrict__ gtab = nullptr) {
+template <int G, int ROWS, int AL, int DEPTH>
+__global__ __launch_bounds__(1024) void k_gprobe(const uint8_t *__restrict__ base, uint64_t n, uint32_t *__restrict__ out) {
     constexpr int PW = 64 / G;
-    // LDSF bit0: allocate + fill the braid kernel's 152 KiB LDS image first; bit1: store 1 u32 per packet
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[(LDSF & 1) ? kLdsWords : 4];
-    if (LDSF & 1) {
-        char *lds = reinterpret_cast<char *>(lds_w);
-        fill_replicated(lds, gtab + OFF_BRAID);
-        fill_ops(lds, gtab + OFF_INV, 6);
-        __syncthreads();
-    }
     constexpr uint32_t RB = 16u * G, kFrame = RB * ROWS;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
     const uint32_t j = lane % G, q = lane / G;
@@ -195,12 +124,8 @@ __global__ __launch_bounds__(1024) void k_gprobe(const uint8_t *__restrict__ bas
         for (int dd = 0; dd < DEPTH; ++dd)
 #pragma unroll
             for (int i = 0; i < ROWS; ++i) acc ^= w[dd][i].x ^ w[dd][i].y ^ w[dd][i].z ^ w[dd][i].w;
-        if (LDSF & 2) {
-            const uint64_t p = r * PW + q;
-            if (j == 0 && p < n) out[p] = acc ^ ((LDSF & 1) ? lds_w[lane] : 0u);
-        }
     }
-    if (acc == 0x12345678u) out[0] = acc ^ ((LDSF & 1) ? lds_w[lane] : 0u);
+    if (acc == 0x12345678u) out[0] = acc;
 }
 
 // Segment layout probe: 16 lanes per packet, lane j owns the contiguous 96-B segment
@@ -301,21 +226,8 @@ int main(int argc, char **argv) {
     vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-#define BV(NAME, FR, VAR, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, FR, DIAG, 1, CrcBEpi, VAR>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
-    BV("var1_oob", 1, 1, 0); BV("var2_xor", 1, 2, 0); BV("var3_both", 1, 3, 0); BV("var0_skel", 1, 0, 3); BV("var1_skel", 1, 1, 3);
-    BV("var4_horner", 1, 4, 0); BV("var6_horner_xor", 1, 6, 0); BV("var7_all", 1, 7, 0); BV("var7_f0", 0, 7, 0);
-    BV("var6_f0", 0, 6, 0); BV("var7_nolut", 1, 7, 1); BV("var7_nocomb", 1, 7, 2); BV("var7_skel", 1, 7, 3); BV("var7_f0_skel", 0, 7, 3);
-    vs.push_back({"new_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 0, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"new_nocomb_d2", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"new_nolut", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"new_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"new_nolut_nocomb", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"braid_f0_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"braid_f1_d1", [&] { hipLaunchKernelGGL((k_fixed_braid<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
-    vs.push_back({"braid_old_rightaligned", [&] { hipLaunchKernelGGL((k_braid_diag<6, 0>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_nolut", [&] { hipLaunchKernelGGL((k_braid_diag<6, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
-    vs.push_back({"braid_nolut_nocomb", [&] { hipLaunchKernelGGL((k_braid_diag<6, 3>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out, s.tabs, cinit); }, {}});
+#define BD(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
+    BD("braid_nolut", 1); BD("braid_nofold", 2); BD("braid_skel", 3);
     vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_nt_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_plain_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, false, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
@@ -332,8 +244,6 @@ int main(int argc, char **argv) {
     vs.push_back({"stage_probe_dma", [&] { hipLaunchKernelGGL((k_stage_probe<1>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
     vs.push_back({"seg_probe_d1", [&] { hipLaunchKernelGGL((k_seg_probe<1>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
     vs.push_back({"seg_probe_d2", [&] { hipLaunchKernelGGL((k_seg_probe<2>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
-#define GPL(G, R, AL, D, F) vs.push_back({"gprobe_G" #G "_R" #R "_al" #AL "_d" #D "_ldsf" #F, [&] { hipLaunchKernelGGL((k_gprobe<G, R, AL, D, F>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out, s.tabs); }, {}})
-    GPL(16, 6, 1, 1, 1); GPL(16, 6, 1, 1, 2); GPL(16, 6, 1, 1, 3); GPL(16, 6, 0, 1, 3);
     vs.push_back({"pieces_fixed", [&] {  // general kernel, fixed provider
         launch_pieces(s, buf, bytes, dev::FixedProvL{1456, 0, 1456u}, n, dev::CrcEpi{out, uint32_t(n)}, nullptr); }, {}});
 
@@ -359,10 +269,16 @@ int main(int argc, char **argv) {
         }
     // sustained: 200 back-to-back launches per selected variant (DVFS steady state)
     if (getenv("KB_SUSTAIN")) {
+        // KB_REPS rounds over the selected variants (interleaved A B C A B C ...), NS
+        // back-to-back launches each; the summary averages the per-round steady medians.
         const int NS = getenv("KB_NS") ? atoi(getenv("KB_NS")) : 200;
+        const int RR = getenv("KB_REPS") ? atoi(getenv("KB_REPS")) : 1;
         std::vector<hipEvent_t> ev(NS + 1);
         for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
-        for (auto &v : vs) {
+        std::vector<std::vector<float>> med(vs.size());
+        for (int rep = 0; rep < RR; ++rep)
+        for (size_t vi = 0; vi < vs.size(); ++vi) {
+            auto &v = vs[vi];
             if (!strstr(getenv("KB_SUSTAIN"), v.name) && strcmp(getenv("KB_SUSTAIN"), "all")) continue;
             CK(hipDeviceSynchronize());
             usleep(200000);  // let clocks settle between variants
@@ -373,11 +289,18 @@ int main(int argc, char **argv) {
             for (int r = 0; r < NS; ++r) { float ms; CK(hipEventElapsedTime(&ms, ev[r], ev[r + 1])); t.push_back(ms); }
             std::vector<float> tail(t.begin() + NS / 2, t.end());
             std::sort(tail.begin(), tail.end());
+            med[vi].push_back(tail[tail.size() / 2]);
             float tot; CK(hipEventElapsedTime(&tot, ev[0], ev[NS]));
             printf("SUSTAIN %-26s all %.1f GB/s | steady median %.4f ms %.1f GB/s | t[0..]=", v.name, bytes * NS / (tot * 1e-3) / 1e9,
                    tail[tail.size() / 2], bytes / (tail[tail.size() / 2] * 1e-3) / 1e9);
             for (int r = 0; r < NS; r += 20) printf("%.0f ", t[r] * 1000);
             printf("us\n");
+        }
+        for (size_t vi = 0; vi < vs.size(); ++vi) {
+            if (med[vi].empty()) continue;
+            double m = 0; for (float x : med[vi]) m += x; m /= med[vi].size();
+            printf("SUMMARY %-26s steady %.4f ms %.1f GB/s (%.1f%% of 8 TB/s) over %zu rounds\n", vs[vi].name, m, bytes / (m * 1e-3) / 1e9,
+                   100.0 * bytes / (m * 1e-3) / 8e12, med[vi].size());
         }
     }
     // back-to-back launches of the production kernel (as bench.py issues them)
@@ -405,7 +328,7 @@ int main(int argc, char **argv) {
         CK(hipMemset(out, 0, n * 4)); vs[bp].f(); CK(hipDeviceSynchronize());
         CK(hipMemcpy(ref.data(), out, n * 4, hipMemcpyDeviceToHost));
         for (auto &v : vs) {
-            if (strncmp(v.name, "var", 3) || strstr(v.name, "skel")) continue;
+            if (strncmp(v.name, "var", 3)) continue;
             CK(hipMemset(out, 0, n * 4)); v.f(); CK(hipDeviceSynchronize());
             CK(hipMemcpy(got.data(), out, n * 4, hipMemcpyDeviceToHost));
             uint64_t bad = 0;

@@ -17,7 +17,7 @@ DEV=$(dirname $(dirname "$HW" 2>/dev/null) 2>/dev/null)
     sleep 0.02
   done ) > $OUT/samples.txt 2>&1 &
 SP=$!
-KB_NS=${KB_NS:-3000} KB_SUSTAIN="${1:-braid_prod,braid_nolut,braid_nolut_nocomb,gprobe_G16_R6_al1_d1_256x1024}" timeout -k 10 200 ./tools/bin/kbench 1048576 2 > $OUT/kbench.log 2>&1
+KB_NS=${KB_NS:-3000} KB_SUSTAIN="${1:-braid_prod,braid_nolut,braid_skel,gprobe_G16_R6_al1_d1_256x1024}" timeout -k 10 200 ./tools/bin/kbench 1048576 2 > $OUT/kbench.log 2>&1
 rc=$?
 kill $SP 2>/dev/null
 grep SUSTAIN $OUT/kbench.log | cut -c1-110
