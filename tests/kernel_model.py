@@ -1,7 +1,9 @@
 """Bit-level CPU model of the two HIP kernels' algorithms (TEST INFRASTRUCTURE).
 
-It mirrors csrc/crc32_kernels.hip step for step — braid tables, x^(-32k) folds,
-cross-lane tree, piece windows, segmented scan — using tables built with the oracle's
+It mirrors csrc/crc32_kernels.hip step for step — braid tables with the next word
+folded into the lookup XOR, the in-lane x^-32 Horner fold, the Horner flush over the
+transposition slot (two halves of 8 columns, x^-1024, masked x^-128 trailing steps),
+piece windows, segmented scan — using tables built with the oracle's
 shift/unshift, so an algebra mistake shows up here, on CPU, before any GPU time.
 It is not the product and is never imported by it.
 """
@@ -71,30 +73,37 @@ def braid_crc(T: Tables, pkt: bytes, addr: int = 0) -> int:
     trail = fs + rows * 256 - (addr + L)  # T: zero bytes after the packet, undone below
     frame = b"\0" * lead + pkt + b"\0" * trail
     assert len(frame) == rows * 256
-    B = [[0, 0, 0, 0] for _ in range(G)]
-    for i in range(rows):
+    # main loop: b <- B ^ w of the current row; b <- T(b) ^ w_next; the last row applies T
+    b = [[int.from_bytes(frame[j * 16 + 4 * k:j * 16 + 4 * k + 4], "little") for k in range(4)] for j in range(G)]
+    for i in range(1, rows):
         for j in range(G):
             c = (i * G + j) * 16
             for k in range(4):
                 w = int.from_bytes(frame[c + 4 * k:c + 4 * k + 4], "little")
-                B[j][k] = _apply(T.braid, B[j][k] ^ w)
-    v = [B[j][0] ^ _apply(T.inv[4], B[j][1]) ^ _apply(T.inv[8], B[j][2] ^ _apply(T.inv[4], B[j][3]))
-         for j in range(G)]
-    d = 1
-    while d < G:
-        nv = list(v)
-        for j in range(G):
-            u = v[j + d] if j + d < G else v[j]
-            if j & (2 * d - 1) == 0:
-                nv[j] = v[j] ^ _apply(T.inv[16 * d], u)
-        v = nv
-        d *= 2
-    r = v[0]
+                b[j][k] = _apply(T.braid, b[j][k]) ^ w
+    b = [[_apply(T.braid, x) for x in bj] for bj in b]
+    # in-lane fold: v_j = b0 ^ x^-32 (b1 ^ x^-32 (b2 ^ x^-32 b3))
+    v = []
+    for j in range(G):
+        x = _apply(T.inv[4], b[j][3]) ^ b[j][2]
+        x = _apply(T.inv[4], x) ^ b[j][1]
+        v.append(_apply(T.inv[4], x) ^ b[j][0])
+    # flush: lane h takes columns 8h .. 8h+7 (Horner with x^-128), h = 1 moved by
+    # x^-1024, both take t masked x^-128 steps (t = trailing zero chunks), then XOR
     t = trail // 16
-    for bit, n in ((1, 16), (2, 32), (4, 64), (8, 128)):
-        if t & bit:
-            r = _apply(T.inv[n], r)
-    return r ^ T.init_const(L)
+    tmax = (rows * 256 - L) // 16
+    halves = []
+    for h in (0, 1):
+        acc = v[8 * h + 7]
+        for jj in range(6, -1, -1):
+            acc = _apply(T.inv[16], acc) ^ v[8 * h + jj]
+        if h:
+            acc = _apply(T.inv[128], acc)
+        for s2 in range(tmax):
+            if s2 < t:
+                acc = _apply(T.inv[16], acc)
+        halves.append(acc)
+    return halves[0] ^ halves[1] ^ T.init_const(L)
 
 
 def pieces_crc(T: Tables, buf: bytes, off: int, L: int) -> int:
