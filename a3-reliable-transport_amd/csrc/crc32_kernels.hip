@@ -32,6 +32,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -57,7 +58,10 @@ constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-
 constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
 constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
 constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
-constexpr uint32_t TAB_WORDS = OFF_HINIT + 68;
+constexpr uint32_t OFF_A16 = OFF_HINIT + 68;          // 4x256 word tables advancing 16 B (k_var_lane)
+constexpr uint32_t OFF_LOPS = OFF_A16 + 1024;         // 3 ops: x^-32, x^-8, shift by 256 B (k_var_lane)
+constexpr uint32_t OFF_LSFF = OFF_LOPS + 3 * 1024;    // shift(~0, m) ^ ~0, m = 0..4096
+constexpr uint32_t TAB_WORDS = OFF_LSFF + 4100;
 
 // LDS images (staggered table sets are described at StagKeys below).
 constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
@@ -750,6 +754,326 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 }
 
 // ------------------------------------------------------------------------------------
+// 2b. k_var_lane — mixed-length batches, one lane per packet part, sorted by size
+// ------------------------------------------------------------------------------------
+// A mixed-length batch (config C5: Zipf lengths, half the packets <= 16 B, a few near
+// 1456 B) is hashed with one lane per TASK: a packet is cut into parts of <= 16 chunks
+// (16-B chunks of the 16-B aligned view) counted back from its last chunk, so no task
+// has more than 16 rows and the waves of a workgroup get balanced work.  Workgroups take
+// segments of up to kLnSeg consecutive packets:
+//   A. offsets/lengths are read (coalesced); tasks get slots by a block-wide scan of the
+//      part counts and are counting-sorted in LDS by their chunk count, largest first.
+//      A segment whose tasks do not fit (long packets) runs in several passes.
+//   B. waves take groups of 64 sorted tasks (snake order over the waves: every wave gets
+//      a similar mix of sizes).  A group of R = max chunks rows is hashed over a frame of
+//      R rows x 16 B per lane, right-aligned at each part's end: rows before the part load
+//      as zeros (out-of-range offsets; leading zeros are free), the packet's bytes before
+//      its start and after its end (head chunk, last row of the last part) are masked.
+//      Each lane runs 4 braids with the 16-B advance tables (staggered, conflict-free):
+//      B_k <- A16(B_k) ^ w_k; the part value P = XOR_k x^(-32k) A16(B_k) goes to LDS.
+//   C. each thread finishes its own packets: Horner over the parts with the 256-B advance,
+//      x^(-8u) for the u bytes after the end in the last chunk, ^ shift(~0, len) ^ ~0.
+// Rows are one stream per wave across its groups: the loads of the next R_BLK rows are
+// issued before the current R_BLK rows are hashed, so small groups still keep R_BLK KiB
+// per wave in flight.  All loads are unconditional (out-of-range offsets for rows outside
+// a part and past the wave's last group) and the row loop has a fixed trip count: the
+// compiler's vmcnt accounting stays counted.  Loads are temporal: a lane reads 16 B of a
+// line per row and the rest of the line in the next rows (nt loads: 2x slower).
+// Algebra model: tests/kernel_model.py (lane_parts, var_lane_group, var_lane_combine).
+constexpr uint32_t kLnSeg = 4096;     // packets per segment (4 per thread)
+constexpr uint32_t kLnTasks = 8192;   // task slots per pass
+constexpr uint32_t kLnPassCap = kLnTasks - 17;  // a pass takes packets whose first task is below this
+constexpr uint32_t kLnOps = 65536;    // plain operators after the staggered region: x^-32, x^-8, A256
+constexpr uint32_t kLnSff = kLnOps + 3 * 4096;   // shift(~0, m) ^ ~0, m = 0..4096
+constexpr uint32_t kLnRec = kLnSff + 4100 * 4;   // task records {view offset, len | j << 13 | slot << 18}
+constexpr uint32_t kLnCnt = kLnRec + kLnTasks * 8;  // 17 class counters, 17 cursors, 16 wave sums, misc
+constexpr uint32_t kLnLdsWords = (kLnCnt + 64 * 4) / 4;
+static_assert(kLnLdsWords * 4 <= 163840, "k_var_lane LDS");
+static_assert(kLnRec % 16 == 0, "record alignment");
+
+// Part value slot t lives in the free half (set 1) of the staggered region's rows.
+__device__ __forceinline__ uint32_t ln_pval_addr(uint32_t t) { return (t >> 5) * 256u + 128u + (t & 31u) * 4u; }
+
+__device__ __forceinline__ uint32_t keep_from_byte(uint32_t b, uint32_t d) {  // keep bytes >= b of dword d
+    const int32_t x = int32_t(8u * b) - int32_t(32u * d);
+    const uint32_t t = uint32_t(x < 0 ? 0 : (x > 32 ? 32 : x));
+    return uint32_t(uint64_t(0xFFFFFFFFu) << t);
+}
+
+template <int R_BLK>
+__global__ __launch_bounds__(1024) void k_var_lane(const uint8_t *__restrict__ view, uint32_t span,
+                                                   const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+                                                   uint32_t lead, uint64_t n, uint32_t seg, uint32_t *__restrict__ out,
+                                                   const uint32_t *__restrict__ gtab, uint32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLnLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    typedef __attribute__((address_space(3))) uint32_t lu32;
+    typedef __attribute__((address_space(3))) u32x2 lu32x2;
+    lchar *const L3 = (lchar *)lds_w;
+    auto lw = [&](uint32_t byte) -> lu32 & { return *(lu32 *)(L3 + byte); };
+    constexpr uint32_t kCls = kLnCnt, kCur = kLnCnt + 17u * 4u, kWs = kLnCnt + 34u * 4u, kMisc = kLnCnt + 50u * 4u;
+    constexpr uint32_t OP_X32 = kLnOps, OP_X8 = kLnOps + 4096u, OP_A256 = kLnOps + 8192u;
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr uint32_t nwave = 16;  // 1024 threads
+    const uint64_t nseg = (n + seg - 1) / seg;
+    if (uint64_t(blockIdx.x) >= nseg) return;
+    const uint32_t *const offlo = reinterpret_cast<const uint32_t *>(offs);  // low dwords: the view is < 2 GiB
+    const __amdgpu_buffer_rsrc_t vs = make_rsrc(view, span);
+    constexpr uint32_t kOOB = 0x80000000u;
+
+    // metadata of one segment: thread tid holds packets tid + 1024 j (buffer loads with
+    // 32-bit offsets from the segment's base: no 64-bit addresses to keep live)
+    uint32_t mo[4], ml[4];
+    auto meta = [&](uint64_t p0, uint32_t cnt) {
+        const __amdgpu_buffer_rsrc_t ro = make_rsrc(offlo + 2 * p0, 8u * cnt);
+        const __amdgpu_buffer_rsrc_t rl = make_rsrc(lens + p0, 4u * cnt);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = tid + 1024u * j;
+            mo[j] = __builtin_amdgcn_raw_buffer_load_b32(ro, int(8u * i), 0, 0);  // out of range: 0
+            ml[j] = __builtin_amdgcn_raw_buffer_load_b32(rl, int(4u * i), 0, 0);
+        }
+    };
+    uint64_t s = blockIdx.x;
+    meta(s * seg, uint32_t(std::min<uint64_t>(seg, n - s * seg)));
+    fill_stag(lds, 0, 0, gtab + OFF_A16);
+    {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_LOPS);
+        for (uint32_t i = tid; i < 3u * 256u; i += blockDim.x) *(lu32x4 *)(L3 + kLnOps + 16u * i) = src[i];
+        for (uint32_t i = tid; i <= kMaxVarLen; i += blockDim.x) lw(kLnSff + 4u * i) = gtab[OFF_LSFF + i];
+    }
+    const StagKeys K(lane);
+
+    for (; s < nseg; s += gridDim.x) {
+        const uint64_t p0 = s * seg;
+        const uint32_t cnt = uint32_t(std::min<uint64_t>(seg, n - p0));
+        const __amdgpu_buffer_rsrc_t ro_out = make_rsrc(out + p0, 4u * cnt);
+        // ---- A. packets -> parts; task slots by a block-wide scan of the part counts ----
+        // per packet: pk = len | parts << 13 | u << 18 (u: bytes after the end in its last
+        // chunk), ts = first task slot; the view offset only lives through phase A
+        uint32_t vo[4], pk[4], ts[4], tsum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = tid + 1024u * j;
+            uint32_t len = ml[j];
+            vo[j] = lead + mo[j];
+            if (i < cnt && len > kMaxVarLen) {
+                atomicOr(status, 1u);
+                len = 0;
+            }
+            len = i < cnt ? len : 0u;
+            const uint32_t e = vo[j] + len;
+            const uint32_t c = len ? ((e + 15u) >> 4) - (vo[j] >> 4) : 0u;
+            const uint32_t np = (c + 15u) >> 4;
+            pk[j] = len | (np << 13) | ((((e + 15u) & ~15u) - e) << 18);
+            ts[j] = tsum;
+            tsum += np;
+            if (len == 0u)  // empty (or rejected) payload: crc 0 (past the segment: out of range)
+                __builtin_amdgcn_raw_buffer_store_b32(0u, ro_out, int(4u * i), 0, 0);
+        }
+        auto parts = [&](uint32_t j) { return (pk[j] >> 13) & 31u; };
+        uint32_t incl = tsum;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) lw(kWs + 4u * wave) = incl;
+        __syncthreads();
+        uint32_t wbase = 0, total = 0;
+        for (uint32_t w = 0; w < nwave; ++w) {
+            const uint32_t v = lw(kWs + 4u * w);
+            wbase += w < wave ? v : 0u;
+            total += v;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) ts[j] += wbase + incl - tsum;
+        const uint32_t npass = total ? (total - 1u) / kLnPassCap + 1u : 0u;
+
+        for (uint32_t pass = 0; pass < npass; ++pass) {
+            const uint32_t tb = pass * kLnPassCap;
+            auto in_pass = [&](uint32_t j) { return parts(j) != 0u && ts[j] >= tb && ts[j] < tb + kLnPassCap; };
+            if (tid < 34u) lw(kCls + 4u * tid) = 0u;
+            __syncthreads();
+            // count tasks per class (rows = chunks of the part: 16, except the head part)
+            auto head_rows = [&](uint32_t j) {
+                const uint32_t len = pk[j] & 0x1FFFu, c = ((vo[j] + len + 15u) >> 4) - (vo[j] >> 4);
+                return c - 16u * (parts(j) - 1u);
+            };
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                if (in_pass(j)) {
+                    atomicAdd((uint32_t *)(lds + kCls + 4u * head_rows(j)), 1u);
+                    if (parts(j) > 1u) atomicAdd((uint32_t *)(lds + kCls + 4u * 16u), parts(j) - 1u);
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {  // class bases, largest class first
+                uint32_t b = 0;
+                for (uint32_t q = 16; q >= 1; --q) {
+                    lw(kCur + 4u * q) = b;
+                    b += lw(kCls + 4u * q);
+                }
+                lw(kMisc) = b;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                if (in_pass(j)) {
+                    const uint32_t hr = head_rows(j);
+                    for (uint32_t k = 0; k < parts(j); ++k) {
+                        const uint32_t pos = atomicAdd((uint32_t *)(lds + kCur + 4u * (k ? 16u : hr)), 1u);
+                        *(lu32x2 *)(L3 + kLnRec + 8u * pos) =
+                            u32x2{vo[j], (pk[j] & 0x1FFFu) | (k << 13) | ((ts[j] - tb + k) << 18)};
+                    }
+                }
+            }
+            __syncthreads();
+
+            // ---- B. rows: one stream per wave over its groups (snake order) ----------------
+            const uint32_t nl = __builtin_amdgcn_readfirstlane(lw(kMisc));
+            const uint32_t ng = (nl + 63u) >> 6;
+            auto group_of = [&](uint32_t k) {  // the wave's k-th group
+                return nwave * k + ((k & 1u) ? nwave - 1u - wave : wave);
+            };
+            // A wave's position in its row stream (k-th group g, row t of cm: uniform) and the
+            // lane's task there: part end ep, part start sp (0x7FFFFFFF: no task), P slot,
+            // byte bounds bnd = lo | hb << 8 (keep bytes >= lo of the head chunk, < hb of the
+            // part's last chunk).
+            struct Side {
+                uint32_t k, g, t, cm;
+                uint32_t ep, sp, slot, bnd;
+            };
+            auto open = [&](Side &S, uint32_t k, bool full) __attribute__((always_inline)) {
+                S.k = k;
+                S.g = group_of(k);
+                S.t = 0;
+                S.cm = 0;
+                if (S.g < ng) {
+                    const uint32_t r = 64u * S.g + lane;
+                    const bool ok = r < nl;
+                    const u32x2 rec = *(const lu32x2 *)(L3 + kLnRec + 8u * (ok ? r : 64u * S.g));
+                    const uint32_t v = rec.x, len = rec.y & 0x1FFFu, pj = (rec.y >> 13) & 31u;
+                    const uint32_t e = v + len, e16 = (e + 15u) & ~15u, off16 = v & ~15u;
+                    const uint32_t m = (((e16 - off16) >> 4) + 15u) >> 4;
+                    S.ep = e16 - 256u * (m - 1u - pj);
+                    const uint32_t sp = pj ? S.ep - 256u : off16;
+                    S.sp = ok ? sp : 0x7FFFFFFFu;
+                    S.cm = __builtin_amdgcn_readfirstlane((S.ep - sp) >> 4);  // lane 0: the group's largest
+                    if (full) {
+                        S.slot = rec.y >> 18;
+                        S.bnd = (pj ? 0u : v & 15u) | ((pj + 1u == m ? 16u - (e16 - e) : 16u) << 8);
+                    }
+                }
+            };
+            // rows of the wave's stream: the row loop gets a fixed trip count
+            uint32_t rows = 0;
+            for (uint32_t k = 0; nwave * k < ng; ++k) {
+                const uint32_t g = group_of(k);
+                if (g >= ng) continue;
+                const u32x2 rec = *(const lu32x2 *)(L3 + kLnRec + 8u * 64u * g);
+                const uint32_t len = rec.y & 0x1FFFu, pj = (rec.y >> 13) & 31u;
+                const uint32_t c = ((rec.x + len + 15u) >> 4) - (rec.x >> 4);
+                rows += pj ? 16u : c - 16u * ((c + 15u) / 16u - 1u);
+            }
+            rows = __builtin_amdgcn_readfirstlane(rows);
+            const uint32_t iters = (rows + 2u * R_BLK - 1u) / (2u * R_BLK);
+
+            Side I, H;
+            open(I, 0, false);
+            open(H, 0, true);
+            uint32_t B0 = 0, B1 = 0, B2 = 0, B3 = 0;
+
+            auto issue_row = [&](u32x4 &w) __attribute__((always_inline)) {
+                if (I.t == I.cm && I.g < ng) open(I, I.k + 1u, false);
+                const int32_t a = int32_t(I.ep) - 16 * int32_t(I.cm - I.t);
+                const uint32_t o = (I.g < ng && a >= int32_t(I.sp)) ? uint32_t(a) : kOOB;
+                w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vs, int(o), 0, 0));
+                ++I.t;
+            };
+            // Past the wave's last group (H.cm = 0) a row is hashed into nothing: no group
+            // end fires.  (An early return there would leave the row's load unconsumed on a
+            // path to the loop's back edge, and the compiler would then wait for every load.)
+            auto hash_row = [&](u32x4 w) __attribute__((always_inline)) {
+                const int32_t a = int32_t(H.ep) - 16 * int32_t(H.cm - H.t);
+                const bool hd = a == int32_t(H.sp);  // this row is the part's first chunk
+                if (__builtin_amdgcn_ballot_w64(hd)) {  // mask the head chunk's bytes before the packet
+                    const uint32_t lo = hd ? H.bnd & 31u : 0u;
+                    w.x &= keep_from_byte(lo, 0);
+                    w.y &= keep_from_byte(lo, 1);
+                    w.z &= keep_from_byte(lo, 2);
+                    w.w &= keep_from_byte(lo, 3);
+                }
+                if (H.t + 1u == H.cm) {  // every part's last chunk: bytes after the packet
+                    const uint32_t hb = H.bnd >> 8;
+                    w.x &= ~keep_from_byte(hb, 0);
+                    w.y &= ~keep_from_byte(hb, 1);
+                    w.z &= ~keep_from_byte(hb, 2);
+                    w.w &= ~keep_from_byte(hb, 3);
+                }
+                if (H.t == 0) {
+                    B0 = w.x;
+                    B1 = w.y;
+                    B2 = w.z;
+                    B3 = w.w;
+                } else {
+                    B0 = stag_apply3x<0>(lds, K.kA, K.sel, B0, w.x);
+                    B1 = stag_apply3x<0>(lds, K.kA, K.sel, B1, w.y);
+                    B2 = stag_apply3x<0>(lds, K.kA, K.sel, B2, w.z);
+                    B3 = stag_apply3x<0>(lds, K.kA, K.sel, B3, w.w);
+                }
+                if (++H.t == H.cm) {  // group end: P = XOR_k x^(-32k) A16(B_k)
+                    uint32_t v = stag_apply3<0>(lds, K.kA, K.sel, B3);
+                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B2);
+                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B1);
+                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B0);
+                    if (H.sp != 0x7FFFFFFFu) lw(ln_pval_addr(H.slot)) = v;
+                    open(H, H.k + 1u, true);
+                }
+            };
+
+            u32x4 A[R_BLK], Bq[R_BLK];
+#pragma unroll
+            for (int r = 0; r < R_BLK; ++r) issue_row(A[r]);
+            for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+                for (int r = 0; r < R_BLK; ++r) issue_row(Bq[r]);
+#pragma unroll
+                for (int r = 0; r < R_BLK; ++r) hash_row(A[r]);
+#pragma unroll
+                for (int r = 0; r < R_BLK; ++r) issue_row(A[r]);
+#pragma unroll
+                for (int r = 0; r < R_BLK; ++r) hash_row(Bq[r]);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stream's trailing out-of-range loads
+            __syncthreads();
+
+            // ---- C. each thread finishes its packets of this pass ---------------------------
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                if (in_pass(j)) {
+                    const uint32_t t0 = ts[j] - tb, u = pk[j] >> 18;
+                    uint32_t acc = lw(ln_pval_addr(t0));
+                    for (uint32_t k = 1; k < parts(j); ++k) acc = op_apply(lds, OP_A256, acc) ^ lw(ln_pval_addr(t0 + k));
+                    for (uint32_t k = 0; k < (u >> 2); ++k) acc = op_apply(lds, OP_X32, acc);
+                    for (uint32_t k = 0; k < (u & 3u); ++k) acc = op_apply(lds, OP_X8, acc);
+                    __builtin_amdgcn_raw_buffer_store_b32(acc ^ lw(kLnSff + 4u * (pk[j] & 0x1FFFu)), ro_out,
+                                                          int(4u * (tid + 1024u * j)), 0, 0);
+                }
+            }
+            __syncthreads();
+        }
+        if (s + gridDim.x < nseg) {  // the next segment's metadata
+            const uint64_t q0 = (s + gridDim.x) * seg;
+            meta(q0, uint32_t(std::min<uint64_t>(seg, n - q0)));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // 3. fused DATA packet builder
 // ------------------------------------------------------------------------------------
 // Stage A: copy chunk i into its wire slot after a 16-B header hole; CRC computed on
@@ -861,6 +1185,11 @@ std::vector<uint32_t> host_tables() {
         make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
     }
     for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
+    make_word_tables(&t[OFF_A16], 16);
+    make_operator(&t[OFF_LOPS], [](uint32_t v) { return unshift_bytes(v, 4); });
+    make_operator(&t[OFF_LOPS + 1024], [](uint32_t v) { return unshift_bytes(v, 1); });
+    make_operator(&t[OFF_LOPS + 2048], [](uint32_t v) { return shift_bytes(v, 256); });
+    for (uint32_t m = 0, v = 0xFFFFFFFFu; m <= kMaxVarLen; ++m, v = shift_bytes(v, 1)) t[OFF_LSFF + m] = v ^ 0xFFFFFFFFu;
     return t;
 }
 
@@ -1148,10 +1477,30 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     if (rc) return rc;
     const uint8_t *b = static_cast<const uint8_t *>(d_base);
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // The piece stream (k_pieces) is the path; WTP_VAR_PATH=lane selects k_var_lane
+    // (section 2b) for A/B measurements.
+    static const bool use_pieces = [] {
+        const char *e = std::getenv("WTP_VAR_PATH");
+        return !(e && std::strcmp(e, "lane") == 0);
+    }();
+    const uint64_t span = (lead + base_bytes + 15) & ~uint64_t(15);
+    if (span >= (1ull << 31))
+        return fail(WTP_EINVAL, "mixed-length view %llu B >= 2 GiB (split the batch)", (unsigned long long)span);
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
-        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
-                           dev::CrcEpi{d_out + p, uint32_t(cnt)}, static_cast<hipStream_t>(stream));
+        if (use_pieces) {
+            rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
+                               dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
+        } else {
+            // segments of <= kLnSeg packets, enough of them to cover every CU
+            const uint64_t seg = std::min<uint64_t>(dev::kLnSeg, std::max<uint64_t>(256, (cnt + s->cus - 1) / s->cus));
+            const uint64_t nseg = (cnt + seg - 1) / seg;
+            const unsigned grid = unsigned(std::min<uint64_t>(nseg, uint64_t(s->cus)));
+            hipLaunchKernelGGL(dev::k_var_lane<4>, dim3(grid), dim3(1024), 0, st, b - lead, uint32_t(span), d_offsets + p,
+                               d_lengths + p, uint32_t(lead), cnt, uint32_t(seg), d_out + p, s->tabs, s->status);
+            rc = launch_check("k_var_lane");
+        }
         if (rc) return rc;
     }
     return WTP_OK;

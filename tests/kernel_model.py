@@ -42,7 +42,7 @@ def _apply(tab: np.ndarray, v: int) -> int:
 class Tables:
     def __init__(self):
         self.braid = _word_tables(BRAID_BLOCK)
-        self.inv = {n: _operator(lambda v, n=n: O.unshift(v, n)) for n in (4, 8, 16, 32, 64, 128)}
+        self.inv = {n: _operator(lambda v, n=n: O.unshift(v, n)) for n in (1, 4, 8, 16, 32, 64, 128)}
         self.s4 = _word_tables(4)
         self.fwd = {d: _operator(lambda v, d=d: O.shift(v, S * d)) for d in (1, 2, 4, 8, 16, 32)}
 
@@ -244,3 +244,84 @@ def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
         p0 = p0n
         rounds += 1
     return out, rounds, hits
+
+
+
+
+def lane_chunks(vo: int, L: int) -> int:
+    """16-B chunks of the (16-B aligned) view a packet touches."""
+    return 0 if L == 0 else ((vo + L + 15) >> 4) - (vo >> 4)
+
+
+def lane_parts(vo: int, L: int):
+    """k_var_lane's tasks for one packet: parts of <= 16 chunks counted back from its last
+    chunk, as (part index j, first chunk address, end address) in the view."""
+    c = lane_chunks(vo, L)
+    m = (c + 15) >> 4
+    e16 = (vo + L + 15) & ~15
+    out = []
+    for j in range(m):
+        ep = e16 - 256 * (m - 1 - j)
+        sp = (vo & ~15) if j == 0 else ep - 256
+        out.append((j, sp, ep))
+    return out
+
+
+class LaneTables:
+    """k_var_lane's tables: 16-B advance word tables (main loop), x^-32, x^-8, the 256-B
+    advance operator (part combine) and shift(~0, m) ^ ~0."""
+
+    def __init__(self):
+        self.a16 = _word_tables(16)
+        self.x32 = _operator(lambda v: O.unshift(v, 4))
+        self.x8 = _operator(lambda v: O.unshift(v, 1))
+        self.a256 = _operator(lambda v: O.shift(v, 256))
+        self.t16 = _operator(lambda v: O.shift(v, 16))
+
+    @staticmethod
+    def sff(m: int) -> int:
+        return O.shift(0xFFFFFFFF, m) ^ 0xFFFFFFFF
+
+
+def var_lane_group(T: LaneTables, view: bytes, tasks):
+    """Phase B of k_var_lane for one group of tasks (vo, L, j, part start, part end): lane
+    i hashes its part over a frame of R = max part chunks rows x 16 B right-aligned at the
+    part's end (rows before the part load as zeros; the packet's head chunk and, in its
+    last part, its last chunk are masked).  4 braids B_k <- A16(B_k) ^ w_k (first row:
+    B_k = w_k); part value P = T16(B0) ^ X(T16(B1) ^ X(T16(B2) ^ X(T16(B3)))), X = x^-32."""
+    R = max((ep - sp) >> 4 for _, _, _, sp, ep in tasks)
+    out = []
+    for vo, L, j, sp, ep in tasks:
+        e = vo + L
+        last = ep >= e
+        B = [0, 0, 0, 0]
+        for t in range(R):
+            a = ep - 16 * (R - t)
+            chunk = bytearray(view[a:a + 16].ljust(16, b"\0")) if a >= sp else bytearray(16)
+            if a == (vo & ~15):
+                for bi in range(vo & 15):
+                    chunk[bi] = 0
+            if t == R - 1 and last:
+                for bi in range(16 - (ep - e), 16):
+                    chunk[bi] = 0
+            w = [int.from_bytes(chunk[4 * k:4 * k + 4], "little") for k in range(4)]
+            B = w if t == 0 else [_apply(T.a16, B[k]) ^ w[k] for k in range(4)]
+        v = _apply(T.t16, B[3])
+        for k in (2, 1, 0):
+            v = _apply(T.t16, B[k]) ^ _apply(T.x32, v)
+        out.append(v)
+    return out
+
+
+def var_lane_combine(T: LaneTables, vo: int, L: int, parts) -> int:
+    """Phase C: Horner over the part values with the 256-B advance, then x^(-8u) for the
+    u bytes after the packet in its last chunk (u>>2 steps of x^-32, u&3 of x^-8)."""
+    acc = parts[0]
+    for p in parts[1:]:
+        acc = _apply(T.a256, acc) ^ p
+    u = ((vo + L + 15) & ~15) - (vo + L)
+    for _ in range(u >> 2):
+        acc = _apply(T.x32, acc)
+    for _ in range(u & 3):
+        acc = _apply(T.x8, acc)
+    return acc ^ T.sff(L)

@@ -76,6 +76,21 @@ def test_fast_path_lengths_and_tails(W, L, n):
     assert np.array_equal(to_u32(out, n), O.batch_fixed(host, stride, L, n))
 
 
+# Horner flush groups: with the full 256-workgroup grid every wave runs 8-round groups;
+# these sizes give each wave several full groups plus a partial one (9 or 10 rounds),
+# exercising the group flush, the end-of-batch partial flush and the last round's
+# packets past n, against the oracle on every packet.
+@pytest.mark.parametrize("L", [1456, 1280, 1296, 528])
+@pytest.mark.parametrize("n", [4 * (4096 * 9 + 1234) + 3, 4 * 4096 * 16 + 1])
+def test_fast_path_full_groups_and_partial_tail(W, L, n):
+    stride = ((L + 15) // 16) * 16
+    host = O.synth_fill_np(n * stride, start_byte=L * 11 + n)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_fixed(d, stride, L, n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_fixed(host, stride, L, n))
+
+
 def test_input_files_through_device(W, golden, golden_dir):
     for name, f in golden["files"].items():
         data = np.frombuffer(open(os.path.join(golden_dir, name), "rb").read(), dtype=np.uint8)
@@ -168,6 +183,62 @@ def test_var_shuffled_offsets_and_empty(W):
     W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
+
+
+# Mixed-length batches through the product path (WTP_VAR_PATH=lane runs the same cases
+# through the k_var_lane A/B variant): large batches with full 4096-packet segments, lengths around the chunk
+# boundaries, unordered/overlapping offsets, empty payloads, an unaligned base.
+@pytest.mark.parametrize("case", ["uniform_shuffled", "all_long_packed", "all_short", "boundary_lengths", "zipf1.0_lead",
+                                  "multi_segment"])
+def test_var_lane_path(W, case):
+    rng = np.random.default_rng(11)
+    n = {"uniform_shuffled": 100_000, "multi_segment": 1_300_000}.get(case, 70_000)
+    lead = 0
+    if case == "uniform_shuffled":
+        lens = rng.integers(0, 1600, n).astype(np.uint32)
+        total = 40_000_000
+        offs = rng.integers(0, total - 1600, n).astype(np.uint64)  # overlapping, unordered
+    else:
+        if case == "all_long_packed":
+            lens = rng.integers(192, 1457, n).astype(np.uint32)
+        elif case == "all_short":
+            lens = rng.integers(0, 192, n).astype(np.uint32)
+        elif case == "boundary_lengths":  # around chunk-count boundaries, up to the 4096-B limit
+            lens = np.array([1, 2, 15, 16, 17, 191, 192, 193, 255, 256, 257, 1505, 1520, 1521, 1536, 1537, 4095,
+                             4096], np.uint32)[rng.integers(0, 18, n)]
+        elif case == "multi_segment":  # > 1 segment per workgroup: the next segment's prefetch
+            lens = O.zipf_lengths(n, s=1.1)
+            lead = 9
+        else:
+            lens = O.zipf_lengths(n, s=1.0)
+            lead = 7
+        offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + np.uint64(3)).astype(np.uint64)
+        total = int(offs[-1] + lens[-1]) + 16
+    host = O.synth_fill_np(lead + total, start_byte=n + lead)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens)), case
+
+
+def test_var_lane_bad_length_sets_status(W):
+    W.device_status(0, clear=True)
+    n = 70_000
+    lens = np.full(n, 700, np.uint32)
+    lens[12345] = 5000
+    offs = (np.arange(n, dtype=np.uint64) * np.uint64(701)).astype(np.uint64)
+    total = int(offs[-1]) + 5001
+    host = O.synth_fill_np(total, start_byte=1)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    got = to_u32(out, n)
+    want = O.batch_var(host, offs, np.where(lens > 4096, 0, lens).astype(np.uint32))
+    want[12345] = 0
+    assert np.array_equal(got, want)
+    assert W.device_status(0, clear=True) & 1
 
 
 def test_var_bad_length_sets_status(W):

@@ -41,7 +41,7 @@ for s in $STEPS; do
              -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
            cd "$ROOT" ;;
     profcfg) cd /tmp && run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$OUT/profcfg" -o cfg -- python3 "$ROOT/tools/bench_configs.py" --only c2,c5,verify --out "$OUT/profcfg_configs.json"
+             -d "$OUT/profcfg" -o cfg -- python3 "$ROOT/tools/bench_configs.py" --only "${CFG_ONLY:-c2,c5,verify}" --out "$OUT/profcfg_configs.json"
            cd "$ROOT" ;;
     extra) run extra 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     cfg)   run cfg 600 python tools/bench_configs.py --only "${CFG_ONLY:-c5,verify}" --out "$OUT/configs.json" ;;
