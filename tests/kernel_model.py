@@ -325,3 +325,86 @@ def var_lane_combine(T: LaneTables, vo: int, L: int, parts) -> int:
     for _ in range(u & 3):
         acc = _apply(T.x8, acc)
     return acc ^ T.sff(L)
+
+
+# ---- k_mixed (mixed-length batches): end-aligned frames, forward operators only -------
+# Short packets (<= MX_TH chunks) run one lane per packet over MX_TH 16-B rows aligned so
+# that every lane's packet ends at the end of the last row; long packets run 16 lanes per
+# packet over R rows x 256 B ending at the packet end.  Loads are unaligned 16-B reads at
+# view offset a; a chunk wholly before the packet start reads zeros (out-of-range offset),
+# the straddling chunk masks the bytes before the start, and a chunk at a negative view
+# offset (a packet starting in the view's first 15 bytes) is loaded at offset 0 and moved
+# up by -a bytes.  Every operator is a forward shift: A256, A16 (= shift by 16 B) and
+# S4 (= shift by 4 B, the slice-by-4 word tables).
+MX_TH = 8
+
+
+class MixedTables:
+    def __init__(self):
+        self.a256 = _word_tables(256)
+        self.a16 = _word_tables(16)
+        self.s4 = _word_tables(4)
+
+
+def mx_chunk(view: bytes, a: int, s: int) -> list[int]:
+    """The 4 words a lane hashes for the chunk at view offset a of a packet starting at
+    s: zeros if the chunk ends at or before s; bytes before s masked."""
+    if a + 16 <= s:
+        return [0, 0, 0, 0]
+    if a < 0:
+        raw = b"\0" * (-a) + view[0:16 + a]  # loaded at 0, moved up by -a bytes
+    else:
+        raw = view[a:a + 16]
+    keep = max(s - a, 0)
+    raw = b"\0" * keep + raw[keep:]
+    return [int.from_bytes(raw[4 * k:4 * k + 4], "little") for k in range(4)]
+
+
+def mx_fold(T: MixedTables, b) -> int:
+    """In-lane fold of the 4 braids: S4(S4(S4(b0) ^ b1) ^ b2) ^ b3 (a data word at the
+    frame's last dword)."""
+    v = b[0]
+    for k in range(1, 4):
+        v = _apply(T.s4, v) ^ b[k]
+    return v
+
+
+def mixed_short_crc(T: MixedTables, view: bytes, s: int, L: int) -> int:
+    e = s + L
+    b = [0, 0, 0, 0]
+    for r in range(MX_TH):
+        w = mx_chunk(view, e - 16 * (MX_TH - r), s)
+        b = [_apply(T.a16, b[k]) ^ w[k] for k in range(4)]
+    return _apply(T.s4, mx_fold(T, b)) ^ Tables.init_const(L)
+
+
+def mx_init_xor(w: list[int], rel: int) -> list[int]:
+    """XOR 0xFF into chunk bytes [rel, rel + 4) (the packet's first 4 bytes, rel = s - a):
+    R_{~0}(M) = R_0(M ^ (~0 || 0^(L-4))) for L >= 4, so no init constant is needed."""
+    out = []
+    for d in range(4):
+        lo = min(max(rel - 4 * d, 0), 4)
+        hi = min(max(rel + 4 - 4 * d, 0), 4)
+        m = ((1 << (8 * hi)) - 1) & ~((1 << (8 * lo)) - 1)
+        out.append(w[d] ^ m)
+    return out
+
+
+def mixed_long_crc(T: MixedTables, view: bytes, s: int, L: int, R: int) -> int:
+    """16 lanes over R >= ceil(L/256) rows (L >= 4); the CRC's initial value is XORed
+    into the packet's first 4 bytes as they are loaded; column values v_j combined by
+    Horner with A16 at the flush, then one S4 (the frame's last dword) and ~."""
+    e = s + L
+    fs = e - 256 * R
+    v = []
+    for j in range(G):
+        b = [0, 0, 0, 0]
+        for i in range(R):
+            a = fs + 256 * i + 16 * j
+            w = mx_init_xor(mx_chunk(view, a, s), s - a)
+            b = [_apply(T.a256, b[k]) ^ w[k] for k in range(4)]
+        v.append(mx_fold(T, b))
+    acc = v[0]
+    for j in range(1, G):
+        acc = _apply(T.a16, acc) ^ v[j]
+    return _apply(T.s4, acc) ^ 0xFFFFFFFF

@@ -222,6 +222,29 @@ def test_var_lane_path(W, case):
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens)), case
 
 
+# Packets starting in the view's first bytes: k_mixed reads the chunk holding such a
+# start at offset 0 and moves it up (no read before the caller's base); every base
+# alignment, short and long lengths, one packet per lane position.
+@pytest.mark.parametrize("lead", [0, 1, 7, 15])
+def test_var_packets_at_view_start(W, lead):
+    lens_set = [1, 5, 15, 16, 17, 100, 127, 128, 129, 255, 256, 257, 300, 1456, 4095, 4096]
+    offs, lens = [], []
+    for L in lens_set:
+        for o in range(0, 20):
+            offs.append(o)
+            lens.append(L)
+    offs = np.array(offs, np.uint64)
+    lens = np.array(lens, np.uint32)
+    n = lens.size
+    total = 4200
+    host = O.synth_fill_np(lead + total, start_byte=lead * 3 + 1)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens))
+
+
 def test_var_lane_bad_length_sets_status(W):
     W.device_status(0, clear=True)
     n = 70_000

@@ -83,3 +83,21 @@ def test_var_lane_model():
             m = len(lane_parts(vo, l))
             assert var_lane_combine(LT, vo, l, vals[k:k + m]) == O.crc32(view[vo:vo + l]), (vo, l)
             k += m
+
+
+def test_mixed_model():
+    """k_mixed's algebra: end-aligned frames with forward operators only, the short
+    (lane per packet) and long (16 lanes, R rows) paths, packets at every start offset
+    including the view's first 15 bytes (negative chunk offsets), extra leading rows."""
+    from kernel_model import MX_TH, MixedTables, mixed_long_crc, mixed_short_crc
+    MT = MixedTables()
+    view = O.synth_fill_np(9000, start_byte=5).tobytes()
+    rng = np.random.default_rng(9)
+    for L in [0, 1, 2, 15, 16, 17, 100, 16 * MX_TH]:
+        for s in list(range(0, 18)) + [int(x) for x in rng.integers(0, 8000, 3)]:
+            assert mixed_short_crc(MT, view, s, L) == O.crc32(view[s:s + L]), (s, L)
+    for L in [4, 5, 17, 65, 129, 255, 256, 257, 700, 1456, 4096]:
+        for s in [0, 1, 7, 12, 13, 14, 15, 16, 33] + [int(x) for x in rng.integers(0, 4800, 2)]:
+            R = (L + 255) // 256
+            for extra in (0, 1):
+                assert mixed_long_crc(MT, view, s, L, R + extra) == O.crc32(view[s:s + L]), (s, L, extra)
