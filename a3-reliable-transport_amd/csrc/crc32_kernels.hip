@@ -86,6 +86,24 @@ typedef __attribute__((address_space(3))) u32x4 lu32x4;
 typedef __attribute__((address_space(3))) u32x2 lu32x2;
 typedef __attribute__((address_space(3))) uint8_t lu8;
 
+// Per-wave phase timestamps for tools/pprobe.hip (built with -DWTP_PROBE=1 there and
+// compiled out of the product): slot k of wave (block, wave) gets value v, e.g. a
+// 100 MHz s_memrealtime stamp.
+#ifndef WTP_PROBE
+#define WTP_PROBE 0
+#endif
+#if WTP_PROBE
+__device__ uint64_t *g_probe;
+#define PC_PROBE(k, v)                                                                                  \
+    do {                                                                                                \
+        if (lane == 0u) g_probe[(uint64_t(blockIdx.x) * 16u + wave) * 8u + (k)] = (v);                 \
+    } while (0)
+#else
+#define PC_PROBE(k, v) \
+    do {               \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
@@ -183,6 +201,23 @@ __device__ __forceinline__ uint32_t stag_apply3(const char *lds, const uint32_t 
     const uint32_t a2 = __builtin_amdgcn_perm(x, key[2], sel[2]);
     const uint32_t a3 = __builtin_amdgcn_perm(x, key[3], sel[3]);
     return xor3(lds_rd(lds, a0 + OFF), lds_rd(lds, a1 + OFF), lds_rd(lds, a2 + OFF)) ^ lds_rd(lds, a3 + OFF);
+}
+
+// Wave issue priority, rotated (general kernel).  The SIMD arbiter favours the oldest of
+// equal-priority waves: with static per-wave work, the four waves sharing a SIMD ran at
+// unequal speeds (k_pieces on C5: 2.8 us per round for the oldest, 4.2 us for the
+// youngest; tools/pprobe.py) and the launch waited for the youngest while its SIMD ran
+// nearly empty.  Each wave steps its priority through 0..3 per round (x = round counter
+// + the wave's age rank), so each spends a quarter of its rounds at every level: C5
+// 57.6 -> 54.6 us (interleaved A/B, tools/ab_c5.py).  The braided kernel, at the read
+// ceiling, lost 1% with it (and 2.5% with dynamic per-workgroup group claims).
+__device__ __forceinline__ void rotate_prio(uint32_t x) {
+    switch (x & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
 }
 
 // Epilogues of the braided kernel.  A flush hands lane 2P + h (h = 0) the result of
@@ -444,6 +479,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     fill_stag(lds, 1, 0, gtab + OFF_INV + 2 * 1024);  // x^-128
     fill_stag(lds, 1, 1, gtab + OFF_INV + 5 * 1024);  // x^-1024
     __syncthreads();
+    PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
 
     // 2-way unrolled: one round in flight while the previous one is hashed, no register
     // copies between the two sets.  (A variant keeping two rounds in flight, with the
@@ -459,6 +495,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
         r += rstep;
     }
     if (k) flush(0, false);
+    PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------------------------
@@ -517,7 +554,8 @@ constexpr uint32_t kPcStage = kPcHinit + 272;
 constexpr uint32_t kPcChunks = 272;  // span chunks a slot holds: 64 pieces + gaps + head slack
 constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read one chunk past
 constexpr uint32_t kPcFlags = kPcStage + 16 * kPcSlot;  // 64 B per wave: packet-start flags
-constexpr uint32_t kPcLdsWords = (kPcFlags + 16 * 64) / 4;  // 161,552 B
+constexpr uint32_t kPcBal = kPcFlags + 16 * 64;          // wave split: 16 piece sums, 17 u64 starts
+constexpr uint32_t kPcLdsWords = (kPcBal + 64 + 17 * 8) / 4;  // 161,752 B
 static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
 static_assert(kPcLdsWords * 4 <= 163840, "LDS");
 
@@ -535,6 +573,99 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
     v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false));
     return v;
 }
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))))) |
+           (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))))) << 32);
+}
+
+// Pieces of packet p as the main loop counts them (an empty or over-long packet is one).
+template <class Prov>
+__device__ __forceinline__ uint32_t piece_count_of(const Prov &prov, const MetaRaw &r) {
+    uint64_t off;
+    uint32_t len, aux = 0, os = 0;
+    bool ok;
+    prov.decode(r, off, len, ok, aux, os);
+    return (len == 0 || len > kMaxVarLen) ? 1u : (len + kPieceS - 1) / kPieceS;
+}
+template <class Prov>
+__device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p, __amdgpu_buffer_rsrc_t rs) {
+    MetaRaw r{};
+    prov.load(p, r, rs);
+    return piece_count_of(prov, r);
+}
+
+// Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
+// equal packet counts: with Zipf lengths, equal counts left the busiest wave 1.43x the
+// mean number of rounds (C5, s = 1.1) and the launch waited for it.  Each thread owns a
+// contiguous sub-range; load() issues the metadata loads of its first kReg packets (they
+// fly while the LDS tables fill), finish() sums them, a block scan places the sub-ranges,
+// and the thread whose sub-range holds wave w's target (total * w / waves) walks it, from
+// registers, to the first packet at or past the target.  Every thread of the block must
+// call finish() (two barriers).
+struct WaveSplit {
+    static constexpr uint32_t kReg = 8;
+    MetaRaw raw[kReg];
+    uint64_t a, b;
+    template <class Prov>
+    __device__ __forceinline__ void load(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1) {
+        const uint64_t R = g1 - g0;
+        a = g0 + R * threadIdx.x / blockDim.x;
+        b = g0 + R * (threadIdx.x + 1) / blockDim.x;
+#pragma unroll
+        for (uint32_t j = 0; j < kReg; ++j) {
+            raw[j] = MetaRaw{};
+            prov.load(a + j < b ? a + j : g0, raw[j], rs);  // g0 < g1: always a valid packet
+        }
+    }
+    template <class Prov>
+    __device__ __forceinline__ void finish(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1,
+                                           char *lds, uint32_t wave, uint32_t lane, uint64_t &lo, uint64_t &hi) {
+        const uint32_t nw = blockDim.x >> 6;
+        const uint64_t m = b - a;
+        uint32_t k[kReg], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kReg; ++j) {
+            k[j] = j < m ? piece_count_of(prov, raw[j]) : 0u;
+            sum += k[j];
+        }
+        for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p, rs);  // > kReg per thread
+        const uint32_t incl = wave_incl_add(sum);
+        uint32_t *const wsum = reinterpret_cast<uint32_t *>(lds + kPcBal);
+        uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kPcBal + 64);
+        if (lane == 63u) wsum[wave] = incl;
+        if (threadIdx.x == 0) {
+            starts[0] = g0;
+            starts[nw] = g1;
+        }
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t v = wsum[w];
+            before += w < wave ? v : 0u;
+            total += v;
+        }
+        const uint32_t excl = before + incl - sum;
+        for (uint32_t w = 1; w < nw; ++w) {
+            const uint32_t target = uint32_t(uint64_t(total) * w / nw);
+            if (target >= excl && target - excl < sum) {
+                uint32_t pre = excl;
+                uint64_t p = a;
+#pragma unroll
+                for (uint32_t j = 0; j < kReg; ++j) {
+                    const bool step = j < m && pre < target;
+                    pre += step ? k[j] : 0u;
+                    p += step ? 1u : 0u;
+                }
+                while (p < b && pre < target) pre += piece_count(prov, p++, rs);
+                starts[w] = p;
+            }
+        }
+        __syncthreads();
+        lo = uniform64(starts[wave]);
+        hi = uniform64(starts[wave + 1]);
+    }
+};
 
 // Lane-contiguous load of kPcChunks 16-B chunks starting at view offset b16 (16-aligned,
 // may be negative near the buffer start): 4 full wave instructions + 16 lanes of a
@@ -575,10 +706,17 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
     n = prov.count(n);  // device-side count for the fix-up pass
-    {
-        const uint64_t tw = uint64_t(gridDim.x) * (blockDim.x >> 6), w0 = uint64_t(blockIdx.x) * (blockDim.x >> 6);
-        if (n * w0 / tw == n * (w0 + (blockDim.x >> 6)) / tw) return;  // no packets for this block
-    }
+    const uint32_t nw = blockDim.x >> 6;
+    const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
+    const uint64_t g0 = n * w0 / tw, g1 = n * (w0 + nw) / tw;  // this workgroup's packets
+    if (g0 == g1) return;                                       // no packets for this block
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
+    PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
+    WaveSplit split;
+    if constexpr (Prov::kVarLen) split.load(prov, rs, g0, g1);
+    PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
     fill_stag(lds, 0, 0, gtab + OFF_S4);
     fill_stag(lds, 0, 1, gtab + OFF_FWD);
     {
@@ -587,15 +725,17 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         for (uint32_t i = threadIdx.x; i < 5 * 256; i += blockDim.x) dst[i] = src[i];
         if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = gtab[OFF_HINIT + threadIdx.x];
     }
-    __syncthreads();
+    uint64_t lo, hi;
+    if constexpr (Prov::kVarLen) {
+        split.finish(prov, rs, g0, g1, lds, wave, lane, lo, hi);  // its barriers also publish the tables
+    } else {
+        lo = n * (w0 + wave) / tw;
+        hi = n * (w0 + wave + 1) / tw;
+        __syncthreads();
+    }
+    PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
 
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t gw = uint64_t(blockIdx.x) * (blockDim.x >> 6) + wave;
-    const uint64_t tw = uint64_t(gridDim.x) * (blockDim.x >> 6);
-    const uint64_t lo = n * gw / tw, hi = n * (gw + 1) / tw;
     const StagKeys K(lane);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
     lchar *const slot = (lchar *)lds_w + kPcStage + wave * kPcSlot;
     constexpr int32_t kSpanBytes = int32_t(16 * kPcChunks);
     constexpr int32_t kNoSpan = 0x7FFFF000;  // out of range: loads return 0, no traffic
@@ -609,9 +749,11 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     if (lo < hi) meta(lo);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loop entry then matches its back edge
 
+    PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
     uint32_t skip = 0, carry = 0;  // pieces of packet p0 done in earlier rounds, their register
     int32_t spec = kNoSpan;        // view offset of the prefetched span
     u32x4 x[5];
+    uint32_t nrounds = 0;
     for (uint64_t p0 = lo; p0 < hi;) {
         uint64_t off;
         uint32_t len, aux = 0, oslot = 0;
@@ -751,7 +893,12 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
         skip = partial ? last_gp + 1 : 0u;
         p0 = p0n;
+        if (WTP_PROBE && nrounds == 0) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
+        rotate_prio(++nrounds + (wave >> 2));
     }
+    PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
+    PC_PROBE(6, nrounds);
+    PC_PROBE(7, hi - lo);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1674,6 +1821,7 @@ namespace dev {
 // raw words into (offset in the view, length, valid, aux, output slot) when the round
 // uses them.  count(n) is the number of packets (device-side for the fix-up pass).
 struct FixedProvL {
+    static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     uint32_t len;
@@ -1687,6 +1835,7 @@ struct FixedProvL {
     }
 };
 struct ArrayProvL {
+    static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
@@ -1709,6 +1858,7 @@ struct ArrayProvL {
 // the last datagram, reads there return 0 and are never selected) and are
 // funnel-shifted at decode.
 struct DgramProvL {
+    static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
@@ -1734,6 +1884,7 @@ struct DgramProvL {
 // whatever order the atomics left them).  The index load makes this provider's other
 // loads dependent (it only sees the rare short or malformed datagrams).
 struct IdxDgramProvL {
+    static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = true;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
