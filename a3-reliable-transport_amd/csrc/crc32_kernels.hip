@@ -602,16 +602,19 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p, __
 // fly while the LDS tables fill), finish() sums them, a block scan places the sub-ranges,
 // and the thread whose sub-range holds wave w's target (total * w / waves) walks it, from
 // registers, to the first packet at or past the target.  Every thread of the block must
-// call finish() (two barriers).
+// call finish() (two barriers).  k_pieces runs 1024-thread blocks: the divisions by the
+// thread and wave counts are shifts (64-bit divisions by a runtime value cost ~100 VALU
+// each, and the target loop had 15 of them).
 struct WaveSplit {
-    static constexpr uint32_t kReg = 8;
+    static constexpr uint32_t kReg = 8, kThreads = 1024, kWaves = kThreads / 64;
     MetaRaw raw[kReg];
     uint64_t a, b;
     template <class Prov>
     __device__ __forceinline__ void load(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1) {
         const uint64_t R = g1 - g0;
-        a = g0 + R * threadIdx.x / blockDim.x;
-        b = g0 + R * (threadIdx.x + 1) / blockDim.x;
+        a = g0 + ((R * threadIdx.x) >> 10);
+        b = g0 + ((R * (threadIdx.x + 1)) >> 10);
+        static_assert(kThreads == 1024, "shifts above");
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) {
             raw[j] = MetaRaw{};
@@ -621,7 +624,7 @@ struct WaveSplit {
     template <class Prov>
     __device__ __forceinline__ void finish(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1,
                                            char *lds, uint32_t wave, uint32_t lane, uint64_t &lo, uint64_t &hi) {
-        const uint32_t nw = blockDim.x >> 6;
+        constexpr uint32_t nw = kWaves;
         const uint64_t m = b - a;
         uint32_t k[kReg], sum = 0;
 #pragma unroll
@@ -647,7 +650,8 @@ struct WaveSplit {
         }
         const uint32_t excl = before + incl - sum;
         for (uint32_t w = 1; w < nw; ++w) {
-            const uint32_t target = uint32_t(uint64_t(total) * w / nw);
+            const uint32_t target = uint32_t((uint64_t(total) * w) >> 4);
+            static_assert(kWaves == 16, "shift above");
             if (target >= excl && target - excl < sum) {
                 uint32_t pre = excl;
                 uint64_t p = a;
