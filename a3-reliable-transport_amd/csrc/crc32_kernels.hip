@@ -307,8 +307,10 @@ struct BuildBEpi {
 // feeds one of the lane's 4 braids (CRC streams over every 64th dword of the frame,
 // tables advancing 256 B).  B <- T(B ^ w) with the next row's word folded into the
 // lookup XOR.  The 4 braids are folded in-lane, b0 ^ x^-32 (b1 ^ x^-32 (b2 ^ x^-32 b3)),
-// giving one column value v_j per lane; the packet's CRC register is XOR_j x^(-128 j) v_j
-// times x^(-128 t) for its t trailing zero chunks.
+// giving one column value v_j per lane; the packet's CRC register is T applied to
+// XOR_j x^(-128 j) v_j times x^(-128 t) for its t trailing zero chunks (the last row's
+// advance T commutes with the x^-k, so it runs once per packet at the flush instead of
+// once per braid per round: 16 of 108 lookups per round gone).
 //
 // Combine (Horner through LDS): each round writes its 64 column values into the wave's
 // 2 KiB transposition slot at [k][q][j]; every 8 rounds the flush has lane 2P + h read
@@ -417,6 +419,9 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             acc = s2 < t ? y : acc;
         }
         acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(acc), 0xB1, 0xF, 0xF, false));  // lane ^ 1
+        // the advance T past the last row, deferred from the rounds (it commutes with
+        // every x^-k above): once per packet instead of four times per lane per round
+        if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
         epi.put(p, acc, h == 0 && (lane >> 3) < k && rr < rounds && p < n, pre);
         if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
@@ -449,13 +454,8 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
             b2 = stag_apply3x<0>(lds, K.kA, K.sel, b2, w.z);
             b3 = stag_apply3x<0>(lds, K.kA, K.sel, b3, w.w);
         }
-        if (!(DIAG & 1)) {
-            b0 = stag_apply3<0>(lds, K.kA, K.sel, b0);
-            b1 = stag_apply3<0>(lds, K.kA, K.sel, b1);
-            b2 = stag_apply3<0>(lds, K.kA, K.sel, b2);
-            b3 = stag_apply3<0>(lds, K.kA, K.sel, b3);
-        }
-        // braid b = 4j + k holds R_0(frame_b) * x^(32 b): fold with x^-32 (Horner in-lane)
+        // braid b = 4j + k holds R_0(frame_b) * x^(32 b) / T (the last row's advance T is
+        // applied at the flush): fold with x^-32 (Horner in-lane)
         uint32_t v;
         if (DIAG & 2) {
             v = xor3(b0, b1, b2) ^ b3;

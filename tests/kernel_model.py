@@ -81,7 +81,7 @@ def braid_crc(T: Tables, pkt: bytes, addr: int = 0) -> int:
             for k in range(4):
                 w = int.from_bytes(frame[c + 4 * k:c + 4 * k + 4], "little")
                 b[j][k] = _apply(T.braid, b[j][k]) ^ w
-    b = [[_apply(T.braid, x) for x in bj] for bj in b]
+    # (the last row's advance T is deferred to the flush: it commutes with every x^-k)
     # in-lane fold: v_j = b0 ^ x^-32 (b1 ^ x^-32 (b2 ^ x^-32 b3))
     v = []
     for j in range(G):
@@ -103,7 +103,7 @@ def braid_crc(T: Tables, pkt: bytes, addr: int = 0) -> int:
             if s2 < t:
                 acc = _apply(T.inv[16], acc)
         halves.append(acc)
-    return halves[0] ^ halves[1] ^ T.init_const(L)
+    return _apply(T.braid, halves[0] ^ halves[1]) ^ T.init_const(L)
 
 
 def pieces_crc(T: Tables, buf: bytes, off: int, L: int) -> int:
