@@ -823,9 +823,10 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
         for (uint32_t i = 0; i < 4; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
         if (lane < kPcChunks - 256u) *(lu32x4 *)(slot + stage_addr(256u + lane)) = x[4];
         __builtin_amdgcn_wave_barrier();
-        // the window's five 16-B blocks, aligned (a dword-aligned variant without the
-        // rotation below was measured 13% slower on C5: its ds_read2_b32 pairs at a
-        // 64-B lane stride conflict 4-way)
+        // the window's five 16-B blocks, aligned (dword-aligned variants without the
+        // rotation below were slower on C5: ds_read2_b32 pairs at the 64-B lane stride
+        // conflict 4-way, +13%; unaligned ds_read_b128 from inline asm, which gfx950
+        // executes correctly, +39%)
         uint32_t d[20];
         {
             const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
