@@ -144,9 +144,10 @@ def test_general_strides_and_alignment(W, L, stride, lead):
     assert np.array_equal(to_u32(out, n), want)
 
 
-def test_zipf_mixed_lengths(W):
-    n = 200_000
-    lens = O.zipf_lengths(n, s=1.1)
+@pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0)])
+def test_zipf_mixed_lengths(W, n, s):
+    """C5 itself at full size (1 M packets, Zipf 1.1 and 1.0), every packet vs the oracle."""
+    lens = O.zipf_lengths(n, s=s)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.sum())
     host = O.synth_fill_np(total)
@@ -155,6 +156,37 @@ def test_zipf_mixed_lengths(W):
     W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
+
+
+def _var_check(W, lens, seed=0):
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    n = int(lens.size)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = max(int(lens.sum()), 1)
+    host = O.synth_fill_np(total, start_byte=seed)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
+
+
+def test_var_wave_split_long_subranges(W):
+    """> 8 packets per thread in a workgroup's wave split (3 M packets: ~11.5 per thread),
+    so the split's non-register fallback loops run; empty packets included."""
+    rng = np.random.default_rng(11)
+    _var_check(W, rng.integers(0, 4, 3 << 20), seed=3)
+
+
+@pytest.mark.parametrize("n", [1, 2, 17, 1000, 1025, 70_000])
+def test_var_wave_split_skewed(W, n):
+    """Piece-balanced wave split with a few 4096-B packets (64 pieces) among 1-B ones:
+    several waves' targets land in one packet (empty waves), and workgroups with fewer
+    packets than threads."""
+    lens = np.ones(n, dtype=np.uint32)
+    lens[:: max(1, n // 7)] = 4096
+    lens[-1] = 4096
+    _var_check(W, lens, seed=n)
 
 
 def test_mixed_golden_digest(W, golden):
