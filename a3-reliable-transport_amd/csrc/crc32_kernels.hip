@@ -7,23 +7,23 @@
 // Two kernel families, both HBM-read-bound integer work (no MFMA):
 //
 // 1. k_fixed_braid<ROWS> — equal-length payloads whose ends are 16-B aligned (the
-//    1456-B DATA chunk case).  16 lanes per packet, 4 packets per wave.  Each lane owns
-//    4 interleaved "braids" (CRC streams over every 64th dword of the packet), so the
-//    16 lanes of a packet read 256 contiguous bytes per row with global_load_dwordx4
-//    (fully coalesced, no LDS staging) and every lane carries 4 independent
-//    dependency chains.  Per dword: one v_perm_b32 builds each LDS address and one
-//    ds_read_b32 fetches the table word; the tables are replicated 32x in LDS so that
-//    lane L always hits bank L%32 (conflict-free random lookups).  At the end the 64
-//    braid registers of a packet are folded with x^(-32b) operators (in-lane, then a
-//    4-step cross-lane tree).
+//    1456-B DATA chunk case, the receiver's 1472-B ring, the fused packet builder).
+//    16 lanes per packet, 4 packets per wave.  Each lane owns 4 interleaved "braids"
+//    (CRC streams over every 64th dword of the packet's frame), so the 16 lanes of a
+//    packet read 256 contiguous bytes per row with buffer_load_dwordx4 (coalesced, no
+//    LDS staging) and every lane carries 4 independent dependency chains.  Per lookup:
+//    one v_perm_b32 builds the LDS address and one ds_read_b32 fetches the table word
+//    from staggered 8-copy tables (conflict-free whatever the data).  A lane folds its
+//    braids in-lane (x^-32 Horner); every 8 rounds a flush combines each packet's 16
+//    columns by Horner's rule through an LDS transposition slot.
 //
 // 2. k_pieces<Prov, Epi> — anything else (mixed lengths, odd strides, unaligned
-//    buffers, receiver verify).  Each packet is cut into pieces of S = 64 bytes
-//    counted back from its end (the head piece is shorter); pieces of consecutive
-//    packets are packed densely into the 64 lanes of a wave ("wavefront-packed
-//    tails"), each lane runs a slice-by-4 chain over its piece (replicated tables),
-//    and a segmented inclusive scan with uniform x^(8*64*d) shifts combines the
-//    pieces of each packet.
+//    buffers, datagrams that are not full ring slots).  Each packet is cut into pieces of
+//    S = 64 bytes counted back from its end (the head piece is shorter); pieces of
+//    consecutive packets are packed densely into the 64 lanes of a wave ("wavefront-
+//    packed tails"), each lane runs a slice-by-4 chain over its piece, and a segmented
+//    inclusive scan with uniform x^(8*64*d) shifts combines the pieces of each packet.
+//    Waves get equal piece counts, and rotate their issue priority.
 //
 // All algebra (tables, operators) is generated on the host in crc32_math.hpp.
 #include <hip/hip_runtime.h>
@@ -58,10 +58,7 @@ constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-
 constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
 constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
 constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
-constexpr uint32_t OFF_A16 = OFF_HINIT + 68;          // 4x256 word tables advancing 16 B (k_var_lane)
-constexpr uint32_t OFF_LOPS = OFF_A16 + 1024;         // 3 ops: x^-32, x^-8, shift by 256 B (k_var_lane)
-constexpr uint32_t OFF_LSFF = OFF_LOPS + 3 * 1024;    // shift(~0, m) ^ ~0, m = 0..4096
-constexpr uint32_t TAB_WORDS = OFF_LSFF + 4100;
+constexpr uint32_t TAB_WORDS = OFF_HINIT + 68;
 
 // LDS images (staggered table sets are described at StagKeys below).
 constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
@@ -907,693 +904,6 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
 }
 
 // ------------------------------------------------------------------------------------
-// 2b. k_var_lane — mixed-length batches, one lane per packet part, sorted by size
-// ------------------------------------------------------------------------------------
-// A mixed-length batch (config C5: Zipf lengths, half the packets <= 16 B, a few near
-// 1456 B) is hashed with one lane per TASK: a packet is cut into parts of <= 16 chunks
-// (16-B chunks of the 16-B aligned view) counted back from its last chunk, so no task
-// has more than 16 rows and the waves of a workgroup get balanced work.  Workgroups take
-// segments of up to kLnSeg consecutive packets:
-//   A. offsets/lengths are read (coalesced); tasks get slots by a block-wide scan of the
-//      part counts and are counting-sorted in LDS by their chunk count, largest first.
-//      A segment whose tasks do not fit (long packets) runs in several passes.
-//   B. waves take groups of 64 sorted tasks (snake order over the waves: every wave gets
-//      a similar mix of sizes).  A group of R = max chunks rows is hashed over a frame of
-//      R rows x 16 B per lane, right-aligned at each part's end: rows before the part load
-//      as zeros (out-of-range offsets; leading zeros are free), the packet's bytes before
-//      its start and after its end (head chunk, last row of the last part) are masked.
-//      Each lane runs 4 braids with the 16-B advance tables (staggered, conflict-free):
-//      B_k <- A16(B_k) ^ w_k; the part value P = XOR_k x^(-32k) A16(B_k) goes to LDS.
-//   C. each thread finishes its own packets: Horner over the parts with the 256-B advance,
-//      x^(-8u) for the u bytes after the end in the last chunk, ^ shift(~0, len) ^ ~0.
-// Rows are one stream per wave across its groups: the loads of the next R_BLK rows are
-// issued before the current R_BLK rows are hashed, so small groups still keep R_BLK KiB
-// per wave in flight.  All loads are unconditional (out-of-range offsets for rows outside
-// a part and past the wave's last group) and the row loop has a fixed trip count: the
-// compiler's vmcnt accounting stays counted.  Loads are temporal: a lane reads 16 B of a
-// line per row and the rest of the line in the next rows (nt loads: 2x slower).
-// Algebra model: tests/kernel_model.py (lane_parts, var_lane_group, var_lane_combine).
-constexpr uint32_t kLnSeg = 4096;     // packets per segment (4 per thread)
-constexpr uint32_t kLnTasks = 8192;   // task slots per pass
-constexpr uint32_t kLnPassCap = kLnTasks - 17;  // a pass takes packets whose first task is below this
-constexpr uint32_t kLnOps = 65536;    // plain operators after the staggered region: x^-32, x^-8, A256
-constexpr uint32_t kLnSff = kLnOps + 3 * 4096;   // shift(~0, m) ^ ~0, m = 0..4096
-constexpr uint32_t kLnRec = kLnSff + 4100 * 4;   // task records {view offset, len | j << 13 | slot << 18}
-constexpr uint32_t kLnCnt = kLnRec + kLnTasks * 8;  // 17 class counters, 17 cursors, 16 wave sums, misc
-constexpr uint32_t kLnLdsWords = (kLnCnt + 64 * 4) / 4;
-static_assert(kLnLdsWords * 4 <= 163840, "k_var_lane LDS");
-static_assert(kLnRec % 16 == 0, "record alignment");
-
-// Part value slot t lives in the free half (set 1) of the staggered region's rows.
-__device__ __forceinline__ uint32_t ln_pval_addr(uint32_t t) { return (t >> 5) * 256u + 128u + (t & 31u) * 4u; }
-
-__device__ __forceinline__ uint32_t keep_from_byte(uint32_t b, uint32_t d) {  // keep bytes >= b of dword d
-    const int32_t x = int32_t(8u * b) - int32_t(32u * d);
-    const uint32_t t = uint32_t(x < 0 ? 0 : (x > 32 ? 32 : x));
-    return uint32_t(uint64_t(0xFFFFFFFFu) << t);
-}
-
-template <int R_BLK>
-__global__ __launch_bounds__(1024) void k_var_lane(const uint8_t *__restrict__ view, uint32_t span,
-                                                   const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-                                                   uint32_t lead, uint64_t n, uint32_t seg, uint32_t *__restrict__ out,
-                                                   const uint32_t *__restrict__ gtab, uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kLnLdsWords];
-    char *lds = reinterpret_cast<char *>(lds_w);
-    typedef __attribute__((address_space(3))) uint32_t lu32;
-    lchar *const L3 = (lchar *)lds_w;
-    auto lw = [&](uint32_t byte) -> lu32 & { return *(lu32 *)(L3 + byte); };
-    constexpr uint32_t kCls = kLnCnt, kCur = kLnCnt + 17u * 4u, kWs = kLnCnt + 34u * 4u, kMisc = kLnCnt + 50u * 4u;
-    constexpr uint32_t OP_X32 = kLnOps, OP_X8 = kLnOps + 4096u, OP_A256 = kLnOps + 8192u;
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr uint32_t nwave = 16;  // 1024 threads
-    const uint64_t nseg = (n + seg - 1) / seg;
-    if (uint64_t(blockIdx.x) >= nseg) return;
-    const uint32_t *const offlo = reinterpret_cast<const uint32_t *>(offs);  // low dwords: the view is < 2 GiB
-    const __amdgpu_buffer_rsrc_t vs = make_rsrc(view, span);
-    constexpr uint32_t kOOB = 0x80000000u;
-
-    // metadata of one segment: thread tid holds packets tid + 1024 j (buffer loads with
-    // 32-bit offsets from the segment's base: no 64-bit addresses to keep live)
-    uint32_t mo[4], ml[4];
-    auto meta = [&](uint64_t p0, uint32_t cnt) {
-        const __amdgpu_buffer_rsrc_t ro = make_rsrc(offlo + 2 * p0, 8u * cnt);
-        const __amdgpu_buffer_rsrc_t rl = make_rsrc(lens + p0, 4u * cnt);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t i = tid + 1024u * j;
-            mo[j] = __builtin_amdgcn_raw_buffer_load_b32(ro, int(8u * i), 0, 0);  // out of range: 0
-            ml[j] = __builtin_amdgcn_raw_buffer_load_b32(rl, int(4u * i), 0, 0);
-        }
-    };
-    uint64_t s = blockIdx.x;
-    meta(s * seg, uint32_t(std::min<uint64_t>(seg, n - s * seg)));
-    fill_stag(lds, 0, 0, gtab + OFF_A16);
-    {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_LOPS);
-        for (uint32_t i = tid; i < 3u * 256u; i += blockDim.x) *(lu32x4 *)(L3 + kLnOps + 16u * i) = src[i];
-        for (uint32_t i = tid; i <= kMaxVarLen; i += blockDim.x) lw(kLnSff + 4u * i) = gtab[OFF_LSFF + i];
-    }
-    const StagKeys K(lane);
-
-    for (; s < nseg; s += gridDim.x) {
-        const uint64_t p0 = s * seg;
-        const uint32_t cnt = uint32_t(std::min<uint64_t>(seg, n - p0));
-        const __amdgpu_buffer_rsrc_t ro_out = make_rsrc(out + p0, 4u * cnt);
-        // ---- A. packets -> parts; task slots by a block-wide scan of the part counts ----
-        // per packet: pk = len | parts << 13 | u << 18 (u: bytes after the end in its last
-        // chunk), ts = first task slot; the view offset only lives through phase A
-        uint32_t vo[4], pk[4], ts[4], tsum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t i = tid + 1024u * j;
-            uint32_t len = ml[j];
-            vo[j] = lead + mo[j];
-            if (i < cnt && len > kMaxVarLen) {
-                atomicOr(status, 1u);
-                len = 0;
-            }
-            len = i < cnt ? len : 0u;
-            const uint32_t e = vo[j] + len;
-            const uint32_t c = len ? ((e + 15u) >> 4) - (vo[j] >> 4) : 0u;
-            const uint32_t np = (c + 15u) >> 4;
-            pk[j] = len | (np << 13) | ((((e + 15u) & ~15u) - e) << 18);
-            ts[j] = tsum;
-            tsum += np;
-            if (len == 0u)  // empty (or rejected) payload: crc 0 (past the segment: out of range)
-                __builtin_amdgcn_raw_buffer_store_b32(0u, ro_out, int(4u * i), 0, 0);
-        }
-        auto parts = [&](uint32_t j) { return (pk[j] >> 13) & 31u; };
-        uint32_t incl = tsum;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) lw(kWs + 4u * wave) = incl;
-        __syncthreads();
-        uint32_t wbase = 0, total = 0;
-        for (uint32_t w = 0; w < nwave; ++w) {
-            const uint32_t v = lw(kWs + 4u * w);
-            wbase += w < wave ? v : 0u;
-            total += v;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) ts[j] += wbase + incl - tsum;
-        const uint32_t npass = total ? (total - 1u) / kLnPassCap + 1u : 0u;
-
-        for (uint32_t pass = 0; pass < npass; ++pass) {
-            const uint32_t tb = pass * kLnPassCap;
-            auto in_pass = [&](uint32_t j) { return parts(j) != 0u && ts[j] >= tb && ts[j] < tb + kLnPassCap; };
-            if (tid < 34u) lw(kCls + 4u * tid) = 0u;
-            __syncthreads();
-            // count tasks per class (rows = chunks of the part: 16, except the head part)
-            auto head_rows = [&](uint32_t j) {
-                const uint32_t len = pk[j] & 0x1FFFu, c = ((vo[j] + len + 15u) >> 4) - (vo[j] >> 4);
-                return c - 16u * (parts(j) - 1u);
-            };
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                if (in_pass(j)) {
-                    atomicAdd((uint32_t *)(lds + kCls + 4u * head_rows(j)), 1u);
-                    if (parts(j) > 1u) atomicAdd((uint32_t *)(lds + kCls + 4u * 16u), parts(j) - 1u);
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {  // class bases, largest class first
-                uint32_t b = 0;
-                for (uint32_t q = 16; q >= 1; --q) {
-                    lw(kCur + 4u * q) = b;
-                    b += lw(kCls + 4u * q);
-                }
-                lw(kMisc) = b;
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                if (in_pass(j)) {
-                    const uint32_t hr = head_rows(j);
-                    for (uint32_t k = 0; k < parts(j); ++k) {
-                        const uint32_t pos = atomicAdd((uint32_t *)(lds + kCur + 4u * (k ? 16u : hr)), 1u);
-                        *(lu32x2 *)(L3 + kLnRec + 8u * pos) =
-                            u32x2{vo[j], (pk[j] & 0x1FFFu) | (k << 13) | ((ts[j] - tb + k) << 18)};
-                    }
-                }
-            }
-            __syncthreads();
-
-            // ---- B. rows: one stream per wave over its groups (snake order) ----------------
-            const uint32_t nl = __builtin_amdgcn_readfirstlane(lw(kMisc));
-            const uint32_t ng = (nl + 63u) >> 6;
-            auto group_of = [&](uint32_t k) {  // the wave's k-th group
-                return nwave * k + ((k & 1u) ? nwave - 1u - wave : wave);
-            };
-            // A wave's position in its row stream (k-th group g, row t of cm: uniform) and the
-            // lane's task there: part end ep, part start sp (0x7FFFFFFF: no task), P slot,
-            // byte bounds bnd = lo | hb << 8 (keep bytes >= lo of the head chunk, < hb of the
-            // part's last chunk).
-            struct Side {
-                uint32_t k, g, t, cm;
-                uint32_t ep, sp, slot, bnd;
-            };
-            auto open = [&](Side &S, uint32_t k, bool full) __attribute__((always_inline)) {
-                S.k = k;
-                S.g = group_of(k);
-                S.t = 0;
-                S.cm = 0;
-                if (S.g < ng) {
-                    const uint32_t r = 64u * S.g + lane;
-                    const bool ok = r < nl;
-                    const u32x2 rec = *(const lu32x2 *)(L3 + kLnRec + 8u * (ok ? r : 64u * S.g));
-                    const uint32_t v = rec.x, len = rec.y & 0x1FFFu, pj = (rec.y >> 13) & 31u;
-                    const uint32_t e = v + len, e16 = (e + 15u) & ~15u, off16 = v & ~15u;
-                    const uint32_t m = (((e16 - off16) >> 4) + 15u) >> 4;
-                    S.ep = e16 - 256u * (m - 1u - pj);
-                    const uint32_t sp = pj ? S.ep - 256u : off16;
-                    S.sp = ok ? sp : 0x7FFFFFFFu;
-                    S.cm = __builtin_amdgcn_readfirstlane((S.ep - sp) >> 4);  // lane 0: the group's largest
-                    if (full) {
-                        S.slot = rec.y >> 18;
-                        S.bnd = (pj ? 0u : v & 15u) | ((pj + 1u == m ? 16u - (e16 - e) : 16u) << 8);
-                    }
-                }
-            };
-            // rows of the wave's stream: the row loop gets a fixed trip count
-            uint32_t rows = 0;
-            for (uint32_t k = 0; nwave * k < ng; ++k) {
-                const uint32_t g = group_of(k);
-                if (g >= ng) continue;
-                const u32x2 rec = *(const lu32x2 *)(L3 + kLnRec + 8u * 64u * g);
-                const uint32_t len = rec.y & 0x1FFFu, pj = (rec.y >> 13) & 31u;
-                const uint32_t c = ((rec.x + len + 15u) >> 4) - (rec.x >> 4);
-                rows += pj ? 16u : c - 16u * ((c + 15u) / 16u - 1u);
-            }
-            rows = __builtin_amdgcn_readfirstlane(rows);
-            const uint32_t iters = (rows + 2u * R_BLK - 1u) / (2u * R_BLK);
-
-            Side I, H;
-            open(I, 0, false);
-            open(H, 0, true);
-            uint32_t B0 = 0, B1 = 0, B2 = 0, B3 = 0;
-
-            auto issue_row = [&](u32x4 &w) __attribute__((always_inline)) {
-                if (I.t == I.cm && I.g < ng) open(I, I.k + 1u, false);
-                const int32_t a = int32_t(I.ep) - 16 * int32_t(I.cm - I.t);
-                const uint32_t o = (I.g < ng && a >= int32_t(I.sp)) ? uint32_t(a) : kOOB;
-                w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vs, int(o), 0, 0));
-                ++I.t;
-            };
-            // Past the wave's last group (H.cm = 0) a row is hashed into nothing: no group
-            // end fires.  (An early return there would leave the row's load unconsumed on a
-            // path to the loop's back edge, and the compiler would then wait for every load.)
-            auto hash_row = [&](u32x4 w) __attribute__((always_inline)) {
-                const int32_t a = int32_t(H.ep) - 16 * int32_t(H.cm - H.t);
-                const bool hd = a == int32_t(H.sp);  // this row is the part's first chunk
-                if (__builtin_amdgcn_ballot_w64(hd)) {  // mask the head chunk's bytes before the packet
-                    const uint32_t lo = hd ? H.bnd & 31u : 0u;
-                    w.x &= keep_from_byte(lo, 0);
-                    w.y &= keep_from_byte(lo, 1);
-                    w.z &= keep_from_byte(lo, 2);
-                    w.w &= keep_from_byte(lo, 3);
-                }
-                if (H.t + 1u == H.cm) {  // every part's last chunk: bytes after the packet
-                    const uint32_t hb = H.bnd >> 8;
-                    w.x &= ~keep_from_byte(hb, 0);
-                    w.y &= ~keep_from_byte(hb, 1);
-                    w.z &= ~keep_from_byte(hb, 2);
-                    w.w &= ~keep_from_byte(hb, 3);
-                }
-                if (H.t == 0) {
-                    B0 = w.x;
-                    B1 = w.y;
-                    B2 = w.z;
-                    B3 = w.w;
-                } else {
-                    B0 = stag_apply3x<0>(lds, K.kA, K.sel, B0, w.x);
-                    B1 = stag_apply3x<0>(lds, K.kA, K.sel, B1, w.y);
-                    B2 = stag_apply3x<0>(lds, K.kA, K.sel, B2, w.z);
-                    B3 = stag_apply3x<0>(lds, K.kA, K.sel, B3, w.w);
-                }
-                if (++H.t == H.cm) {  // group end: P = XOR_k x^(-32k) A16(B_k)
-                    uint32_t v = stag_apply3<0>(lds, K.kA, K.sel, B3);
-                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B2);
-                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B1);
-                    v = op_apply(lds, OP_X32, v) ^ stag_apply3<0>(lds, K.kA, K.sel, B0);
-                    if (H.sp != 0x7FFFFFFFu) lw(ln_pval_addr(H.slot)) = v;
-                    open(H, H.k + 1u, true);
-                }
-            };
-
-            u32x4 A[R_BLK], Bq[R_BLK];
-#pragma unroll
-            for (int r = 0; r < R_BLK; ++r) issue_row(A[r]);
-            for (uint32_t it = 0; it < iters; ++it) {
-#pragma unroll
-                for (int r = 0; r < R_BLK; ++r) issue_row(Bq[r]);
-#pragma unroll
-                for (int r = 0; r < R_BLK; ++r) hash_row(A[r]);
-#pragma unroll
-                for (int r = 0; r < R_BLK; ++r) issue_row(A[r]);
-#pragma unroll
-                for (int r = 0; r < R_BLK; ++r) hash_row(Bq[r]);
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stream's trailing out-of-range loads
-            __syncthreads();
-
-            // ---- C. each thread finishes its packets of this pass ---------------------------
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                if (in_pass(j)) {
-                    const uint32_t t0 = ts[j] - tb, u = pk[j] >> 18;
-                    uint32_t acc = lw(ln_pval_addr(t0));
-                    for (uint32_t k = 1; k < parts(j); ++k) acc = op_apply(lds, OP_A256, acc) ^ lw(ln_pval_addr(t0 + k));
-                    for (uint32_t k = 0; k < (u >> 2); ++k) acc = op_apply(lds, OP_X32, acc);
-                    for (uint32_t k = 0; k < (u & 3u); ++k) acc = op_apply(lds, OP_X8, acc);
-                    __builtin_amdgcn_raw_buffer_store_b32(acc ^ lw(kLnSff + 4u * (pk[j] & 0x1FFFu)), ro_out,
-                                                          int(4u * (tid + 1024u * j)), 0, 0);
-                }
-            }
-            __syncthreads();
-        }
-        if (s + gridDim.x < nseg) {  // the next segment's metadata
-            const uint64_t q0 = (s + gridDim.x) * seg;
-            meta(q0, uint32_t(std::min<uint64_t>(seg, n - q0)));
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// 2c. k_mixed — mixed-length batches: short packets one lane each, long packets 16 lanes
-// ------------------------------------------------------------------------------------
-// A wave takes segments of 64 consecutive packets (lane l: packet 64 seg + l).
-//   Short pass: packets of <= TH 16-B chunks run one lane per packet over TH rows.  Row r
-//     of a lane reads the chunk ending 16 (TH - 1 - r) bytes before its packet's end, so
-//     every lane's packet ends with the last row and rows before a packet read zeros
-//     (out-of-range offset; leading zeros are free, R_0(0^k || M) = R_0(M)).  Rows no lane
-//     needs are skipped (wave-uniform).  4 braids per lane advance by A16 (shift by 16 B).
-//   Long pass: the other packets are listed in LDS in lane order and taken 4 per round,
-//     16 lanes each, over R rows x 256 B ending at the packet end (R = the round's largest
-//     ceil(len/256), wave-uniform), braids advancing by A256 — the braided kernel's row
-//     shape on unaligned frames.  The rows of the segment's rounds form one stream: the
-//     loads of the next RB rows are issued before the current RB rows are hashed.  Each
-//     round's 64 column values go to the wave's transposition slot; at 8 rounds (or the
-//     segment end) lane 4k + q evaluates packet (k, q) by Horner's rule with A16.
-// Loads are unaligned 16-B buffer reads at the chunk's view offset a, so a frame ends
-// exactly at its packet's end and no trailing-zero fix is needed; the chunk holding the
-// packet start has its earlier bytes masked.  A chunk at a negative view offset (packet
-// starting in the view's first 15 bytes) is read at offset 0 and moved up by -a bytes.
-// Only forward operators are used: A256, S4 (shift by 4 B: the in-lane fold and the last
-// dword) and A16 — three staggered table sets (LDS region 0 = {A256, S4}, region 1 set 0 =
-// A16; the free set-1 halves of region 1 hold the 16 waves' 2 KiB slots).  crc =
-// S4(fold) ^ shift(~0, len) ^ ~0, the constant gathered from a global table.
-// Algebra model: tests/kernel_model.py (mixed_short_crc, mixed_long_crc).
-constexpr uint32_t kMxList = 131072;  // per wave: 3 long lists of 64 x {e, len | rows << 13 | lane << 18}
-constexpr uint32_t kMxLdsWords = (kMxList + 16 * 1536) / 4;  // 155,648 B
-static_assert(kMxLdsWords * 4 <= 163840, "k_mixed LDS");
-
-__device__ __forceinline__ uint32_t mx_slot_addr(uint32_t wave, uint32_t wi) {  // slot word wi of a wave
-    return 65536u + (16u * wave + (wi >> 5)) * 256u + 128u + (wi & 31u) * 4u;
-}
-
-// Zero the bytes of a 16-B chunk before byte rel (rel <= 0: keep all, >= 16: none).
-__device__ __forceinline__ u32x4 mask_before(u32x4 w, int32_t rel) {
-    const uint32_t r = uint32_t(rel < 0 ? 0 : (rel > 16 ? 16 : rel));
-    w.x &= keep_from_byte(r, 0);
-    w.y &= keep_from_byte(r, 1);
-    w.z &= keep_from_byte(r, 2);
-    w.w &= keep_from_byte(r, 3);
-    return w;
-}
-
-// XOR 0xFF into chunk bytes [rel, rel + 4): the packet's first 4 bytes (rel = s - a).
-// R_{~0}(M) = R_0(M ^ (~0 || 0^(L-4))) for L >= 4, so long packets need no init constant.
-__device__ __forceinline__ u32x4 init_xor(u32x4 w, int32_t rel) {
-    auto m = [&](int32_t d) {
-        const int32_t lo = rel - 4 * d, hi = lo + 4;
-        const uint32_t l = uint32_t(lo < 0 ? 0 : (lo > 4 ? 4 : lo)), h = uint32_t(hi < 0 ? 0 : (hi > 4 ? 4 : hi));
-        return uint32_t((uint64_t(1) << (8u * h)) - 1u) & ~uint32_t((uint64_t(1) << (8u * l)) - 1u);
-    };
-    w.x ^= m(0);
-    w.y ^= m(1);
-    w.z ^= m(2);
-    w.w ^= m(3);
-    return w;
-}
-
-// A chunk loaded at offset 0 for view offset a in (-16, 0): move its bytes up by -a.
-__device__ __forceinline__ u32x4 move_up(u32x4 w, int32_t a) {
-    const uint32_t k = uint32_t(-a);
-    uint64_t lo = (uint64_t(w.y) << 32) | w.x, hi = (uint64_t(w.w) << 32) | w.z;
-    if (k >= 8) {
-        hi = lo << (8u * (k - 8u));
-        lo = 0;
-    } else if (k) {
-        hi = (hi << (8u * k)) | (lo >> (64u - 8u * k));
-        lo <<= 8u * k;
-    }
-    return u32x4{uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
-}
-
-template <uint32_t TH, int RB, int DIAG = 0>
-__global__ __launch_bounds__(1024) void k_mixed(const uint8_t *__restrict__ view, uint32_t span,
-                                                const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-                                                uint64_t n, uint32_t *__restrict__ out,
-                                                const uint32_t *__restrict__ gtab, uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kMxLdsWords];
-    char *lds = reinterpret_cast<char *>(lds_w);
-    typedef __attribute__((address_space(3))) uint32_t lu32;
-    lchar *const L3 = (lchar *)lds_w;
-    constexpr uint32_t kOOB = 0x80000000u;
-    constexpr uint32_t kGroup = 8;        // rounds per slot flush
-    constexpr uint32_t kPad = 2u * RB;    // long rows per segment at least (see the stream)
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t j = lane & 15u, q = lane >> 4;
-    const uint32_t nseg = uint32_t((n + 63) >> 6);
-    const uint32_t tw = gridDim.x * 16u, gw = blockIdx.x * 16u + wave;
-    const uint32_t nmine = gw < nseg ? (nseg - gw + tw - 1u) / tw : 0u;  // this wave's segments gw + m tw
-    const __amdgpu_buffer_rsrc_t vs = make_rsrc(view, span);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(offs, uint32_t(8 * n));  // n < 2^28 (host sub-batches)
-    const __amdgpu_buffer_rsrc_t rl = make_rsrc(lens, uint32_t(4 * n));
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(out, uint32_t(4 * n));
-    const __amdgpu_buffer_rsrc_t rtab = make_rsrc(gtab + OFF_LSFF, 4u * (kMaxVarLen + 1u));
-    auto seg_of = [&](uint32_t m) { return gw + m * tw; };  // >= nseg: past the wave's last
-
-    uint32_t m_off = 0, m_len = 0;  // raw metadata of the next segment to decode
-    auto meta = [&](uint32_t sg) {   // packet 64 sg + lane: low offset dword (view < 2 GiB), length
-        const uint32_t p = sg * 64u + lane;
-        const bool in = sg < nseg;
-        m_off = __builtin_amdgcn_raw_buffer_load_b32(ro, int(in ? 8u * p : kOOB), 0, 0);
-        m_len = __builtin_amdgcn_raw_buffer_load_b32(rl, int(in ? 4u * p : kOOB), 0, 0);
-    };
-    uint32_t d_e = 0, d_s = 0, d_len = 0, d_cinit = 0;  // decoded segment (this lane's packet)
-    bool d_valid = false;
-    auto decode = [&](uint32_t sg) {
-        d_valid = sg < nseg && uint64_t(sg) * 64u + lane < n;
-        uint32_t len = m_len;
-        if (d_valid && len > kMaxVarLen) {
-            atomicOr(status, 1u);
-            len = 0;
-        }
-        d_len = d_valid ? len : 0u;
-        d_s = m_off;
-        d_e = d_s + d_len;
-        d_cinit = __builtin_amdgcn_raw_buffer_load_b32(rtab, int(4u * d_len), 0, 0);  // shift(~0, len) ^ ~0
-    };
-    u32x4 ws[TH];
-    auto issue_short = [&]() {  // row r: the chunk ending 16 (TH - 1 - r) bytes before the packet end
-        const uint32_t c = (d_len + 15u) >> 4, cs = c > TH ? 0u : c;
-#pragma unroll
-        for (uint32_t r = 0; r < TH; ++r) {
-            const int32_t a = int32_t(d_e) - int32_t(16u * (TH - r));
-            const uint32_t o = r + cs >= TH ? (a < 0 ? 0u : uint32_t(a)) : kOOB;
-            ws[r] = buf_ld16(vs, o);
-        }
-    };
-
-    // ---- long lists: three per wave (the hash cursor may still be in segment m-1 while
-    // segment m+1's list is built); per list the round rows (lane r: rows of round r), the
-    // packet and round counts and the segment number --------------------------------------
-    uint32_t Rr0 = 0, Rr1 = 0, Rr2 = 0, nl0 = 0, nl1 = 0, nl2 = 0, nr0 = 0, nr1 = 0, nr2 = 0, sg0 = 0, sg1 = 0, sg2 = 0;
-    auto pick = [](uint32_t b, uint32_t x0, uint32_t x1, uint32_t x2) { return b == 0 ? x0 : (b == 1 ? x1 : x2); };
-    auto list_at = [&](uint32_t b) { return L3 + kMxList + wave * 1536u + b * 512u; };
-    // entries {e, len | rows << 13 | lane << 18}, sorted by rows (largest first); a list
-    // with fewer than kPad rows gets its last round (or an empty round) lengthened: extra
-    // leading rows read zeros (free)
-    auto build_list = [&](uint32_t b, uint32_t sg) {
-        const bool lng = d_len > 16u * TH;
-        const uint32_t rows = (d_len + 255u) >> 8;
-        const uint64_t lb = __builtin_amdgcn_ballot_w64(lng);
-        const uint32_t nl = uint32_t(__builtin_popcountll(lb));
-        uint32_t pos = 0, cum = 0;
-        for (uint32_t v = kMaxVarLen / 256u; v >= 1u && cum < nl; --v) {
-            const uint64_t mk = __builtin_amdgcn_ballot_w64(lng && rows == v);
-            if (lng && rows == v)
-                pos = cum + __builtin_amdgcn_mbcnt_hi(uint32_t(mk >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mk), 0u));
-            cum += uint32_t(__builtin_popcountll(mk));
-        }
-        lchar *const lst = list_at(b);
-        if (lng) *(lu32x2 *)(lst + 8u * pos) = u32x2{d_e, d_len | (rows << 13) | (lane << 18)};
-        __builtin_amdgcn_wave_barrier();
-        uint32_t nr = (nl + 3u) >> 2;
-        uint32_t Rr = lane < nr ? ((*(lu32 *)(lst + 32u * lane + 4u)) >> 13) & 31u : 0u;
-        const uint32_t total = __builtin_amdgcn_readlane(wave_incl_add(Rr), 63);
-        if (total < kPad) {
-            if (nr == 0u) nr = 1u;
-            if (lane == nr - 1u) Rr += kPad - total;
-        }
-        Rr0 = b == 0 ? Rr : Rr0;
-        Rr1 = b == 1 ? Rr : Rr1;
-        Rr2 = b == 2 ? Rr : Rr2;
-        nl0 = b == 0 ? nl : nl0;
-        nl1 = b == 1 ? nl : nl1;
-        nl2 = b == 2 ? nl : nl2;
-        nr0 = b == 0 ? nr : nr0;
-        nr1 = b == 1 ? nr : nr1;
-        nr2 = b == 2 ? nr : nr2;
-        sg0 = b == 0 ? sg : sg0;
-        sg1 = b == 1 ? sg : sg1;
-        sg2 = b == 2 ? sg : sg2;
-    };
-
-    meta(seg_of(0));
-    fill_stag(lds, 0, 0, gtab + OFF_BRAID);  // A256
-    fill_stag(lds, 0, 1, gtab + OFF_S4);     // S4
-    fill_stag(lds, 1, 0, gtab + OFF_A16);    // A16
-    __syncthreads();
-    if (nmine == 0) return;
-    const StagKeys K(lane);
-    decode(seg_of(0));
-    issue_short();
-    meta(seg_of(1));
-    build_list(0, seg_of(0));
-
-    // ---- the long-row stream: one per wave over all its segments ---------------------
-    // Cursor: list b, round r, row i of the round's R rows, segments entered sc; the lane's
-    // packet end e and start s in that round (e = s = 0: no packet).
-    struct Cur {
-        uint32_t b, r, i, R, sc;
-        uint32_t e, s;
-    };
-    auto open_round = [&](Cur &S) __attribute__((always_inline)) {
-        S.i = 0;
-        S.R = __builtin_amdgcn_readlane(pick(S.b, Rr0, Rr1, Rr2), S.r);
-        const uint32_t idx = 4u * S.r + q;
-        const bool has = idx < pick(S.b, nl0, nl1, nl2);
-        const u32x2 en = *(const lu32x2 *)(list_at(S.b) + 8u * (has ? idx : 0u));
-        S.e = has ? en.x : 0u;
-        S.s = has ? en.x - (en.y & 0x1FFFu) : 0u;
-    };
-    auto next_round = [&](Cur &S) __attribute__((always_inline)) {  // returns through S
-        if (++S.r == pick(S.b, nr0, nr1, nr2)) {
-            S.b = S.b == 2u ? 0u : S.b + 1u;
-            S.r = 0;
-            ++S.sc;
-        }
-        open_round(S);
-    };
-    Cur I{0, 0, 0, 0, 0, 0, 0}, H{0, 0, 0, 0, 0, 0, 0};
-    open_round(I);
-    open_round(H);
-    auto issue_row = [&](u32x4 &w) __attribute__((always_inline)) {
-        if (I.i == I.R) next_round(I);
-        const int32_t a = int32_t(I.e) - int32_t(256u * (I.R - I.i)) + int32_t(16u * j);
-        const bool need = a + 16 > int32_t(I.s);
-        w = buf_ld16(vs, need ? (a < 0 ? 0u : uint32_t(a)) : kOOB);
-        ++I.i;
-    };
-
-    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, k = 0, rbase = 0;
-    // Horner over a round's 16 columns for the rounds in the slot (lane 4 kk + qq: round
-    // rbase + kk, packet qq), then S4 and ~ (the init was folded into the data).
-    auto flush = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t kk = lane >> 2, qq = lane & 3u, idx = 4u * (rbase + kk) + qq;
-        const bool on = lane < 4u * k && idx < pick(H.b, nl0, nl1, nl2);
-        const uint32_t base = kk * 64u + qq * 16u;
-        const u32x4 v0 = *(const lu32x4 *)(L3 + mx_slot_addr(wave, base));
-        const u32x4 v1 = *(const lu32x4 *)(L3 + mx_slot_addr(wave, base + 4u));
-        const u32x4 v2 = *(const lu32x4 *)(L3 + mx_slot_addr(wave, base + 8u));
-        const u32x4 v3 = *(const lu32x4 *)(L3 + mx_slot_addr(wave, base + 12u));
-        uint32_t acc = v0.x;
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v0.y);  // A16 Horner over the 16 columns
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v0.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v0.w);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v1.x);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v1.y);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v1.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v1.w);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v2.x);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v2.y);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v2.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v2.w);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v3.x);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v3.y);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v3.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, v3.w);
-        acc = stag_apply3<128>(lds, K.kA, K.sel, acc);  // S4: the frame's last dword
-        const uint32_t ey = *(const lu32 *)(list_at(H.b) + 8u * (on ? idx : 0u) + 4u);
-        const uint32_t pp = pick(H.b, sg0, sg1, sg2) * 64u + (ey >> 18);
-        __builtin_amdgcn_raw_buffer_store_b32(~acc, rout, int(on ? 4u * pp : kOOB), 0, 0);
-        __builtin_amdgcn_wave_barrier();
-        rbase += k;
-        k = 0;
-    };
-    auto hash_row = [&](u32x4 w) __attribute__((always_inline)) {
-        const int32_t a = int32_t(H.e) - int32_t(256u * (H.R - H.i)) + int32_t(16u * j);
-        const int32_t rel = int32_t(H.s) - a;  // > 0: bytes before the packet start
-        if (__builtin_amdgcn_ballot_w64(a < 0 && rel < 16)) {
-            if (a < 0 && rel < 16) w = move_up(w, a);
-        }
-        if (__builtin_amdgcn_ballot_w64(rel > -4 && rel < 16)) {  // the packet's first 4 bytes
-            w = mask_before(w, rel);
-            w = init_xor(w, rel);
-        }
-        if (H.i == 0) {
-            b0 = w.x;
-            b1 = w.y;
-            b2 = w.z;
-            b3 = w.w;
-        } else if (DIAG & 4) {
-            b0 = (b0 ^ w.x) + (b0 >> 3);
-            b1 = (b1 ^ w.y) + (b1 >> 3);
-            b2 = (b2 ^ w.z) + (b2 >> 3);
-            b3 = (b3 ^ w.w) + (b3 >> 3);
-        } else {
-            b0 = stag_apply3x<0>(lds, K.kA, K.sel, b0, w.x);  // A256
-            b1 = stag_apply3x<0>(lds, K.kA, K.sel, b1, w.y);
-            b2 = stag_apply3x<0>(lds, K.kA, K.sel, b2, w.z);
-            b3 = stag_apply3x<0>(lds, K.kA, K.sel, b3, w.w);
-        }
-        if (++H.i == H.R) {  // round end: column value of this lane
-            uint32_t v = stag_apply3x<128>(lds, K.kA, K.sel, b0, b1);  // S4 fold
-            v = stag_apply3x<128>(lds, K.kA, K.sel, v, b2);
-            v = stag_apply3x<128>(lds, K.kA, K.sel, v, b3);
-            *(lu32 *)(L3 + mx_slot_addr(wave, k * 64u + lane)) = v;
-            ++k;
-            const bool last = H.r + 1u == pick(H.b, nr0, nr1, nr2);
-            if (k == kGroup || last) flush();
-            if (last) rbase = 0;
-            next_round(H);
-        }
-    };
-
-    u32x4 A[RB], Bq[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) issue_row(A[r]);
-
-    // Segment m: short pass of m, then segment m+1 decoded (its list, short rows and
-    // init constants issued, metadata of m+2), then the stream runs until its issue
-    // cursor has entered segment m+1.  The issue cursor runs RB rows ahead of the hash
-    // cursor and moves at most 2 RB rows per iteration, so with every segment at least
-    // 2 RB rows long it never needs a list not yet built.  Iteration nmine drains the
-    // stream (its segment is past the wave's last: an empty padded list).
-    for (uint32_t m = 0; m <= nmine; ++m) {
-        // ---- short pass of segment m: one lane per packet, TH rows ending at its end ----
-        {
-            const uint32_t c = (d_len + 15u) >> 4;
-            const bool lng = c > TH;
-            const uint32_t cs = lng ? 0u : c;
-            uint32_t C = 0;  // rows any lane needs (wave-uniform)
-#pragma unroll
-            for (uint32_t t = TH; t > 0; --t) {
-                if (C == 0 && __builtin_amdgcn_ballot_w64(cs >= t)) C = t;
-            }
-            uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < TH; ++r) {
-                if (r + C < TH) continue;  // no lane has bytes in this row
-                u32x4 w = ws[r];
-                const int32_t a = int32_t(d_e) - int32_t(16u * (TH - r));
-                if (__builtin_amdgcn_ballot_w64(a < 0 && r + cs >= TH)) {
-                    if (a < 0) w = move_up(w, a);
-                }
-                w = mask_before(w, int32_t(d_s) - a);
-                if (r + C == TH) {  // first row hashed: the braids are zero
-                    c0 = w.x;
-                    c1 = w.y;
-                    c2 = w.z;
-                    c3 = w.w;
-                } else {
-                    c0 = stag_apply3x<0>(lds, K.kB, K.sel, c0, w.x);  // A16
-                    c1 = stag_apply3x<0>(lds, K.kB, K.sel, c1, w.y);
-                    c2 = stag_apply3x<0>(lds, K.kB, K.sel, c2, w.z);
-                    c3 = stag_apply3x<0>(lds, K.kB, K.sel, c3, w.w);
-                }
-            }
-            uint32_t v = stag_apply3x<128>(lds, K.kA, K.sel, c0, c1);  // S4 fold
-            v = stag_apply3x<128>(lds, K.kA, K.sel, v, c2);
-            v = stag_apply3x<128>(lds, K.kA, K.sel, v, c3);
-            v = stag_apply3<128>(lds, K.kA, K.sel, v);
-            const uint32_t p = seg_of(m) * 64u + lane;
-            __builtin_amdgcn_raw_buffer_store_b32(v ^ d_cinit, rout, int(d_valid && !lng ? 4u * p : kOOB), 0, 0);
-        }
-        // ---- segment m+1: decode, list, short rows; metadata of m+2 ------------------
-        decode(seg_of(m + 1u));
-        issue_short();
-        meta(seg_of(m + 2u));
-        build_list((m + 1u) % 3u, seg_of(m + 1u));
-        // ---- long rows until the issue cursor enters segment m+1 ----------------------
-        // (a segment holds at most 16 rounds x 16 rows: the cap only bounds a logic error)
-        uint32_t guard = 0;
-        do {
-#pragma unroll
-            for (int r = 0; r < RB; ++r) issue_row(Bq[r]);
-#pragma unroll
-            for (int r = 0; r < RB; ++r) hash_row(A[r]);
-#pragma unroll
-            for (int r = 0; r < RB; ++r) issue_row(A[r]);
-#pragma unroll
-            for (int r = 0; r < RB; ++r) hash_row(Bq[r]);
-        } while (I.sc <= m && ++guard < 512u);
-    }
-}
-
-// ------------------------------------------------------------------------------------
 // 3. fused DATA packet builder
 // ------------------------------------------------------------------------------------
 // Stage A: copy chunk i into its wire slot after a 16-B header hole; CRC computed on
@@ -1705,11 +1015,6 @@ std::vector<uint32_t> host_tables() {
         make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
     }
     for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
-    make_word_tables(&t[OFF_A16], 16);
-    make_operator(&t[OFF_LOPS], [](uint32_t v) { return unshift_bytes(v, 4); });
-    make_operator(&t[OFF_LOPS + 1024], [](uint32_t v) { return unshift_bytes(v, 1); });
-    make_operator(&t[OFF_LOPS + 2048], [](uint32_t v) { return shift_bytes(v, 256); });
-    for (uint32_t m = 0, v = 0xFFFFFFFFu; m <= kMaxVarLen; ++m, v = shift_bytes(v, 1)) t[OFF_LSFF + m] = v ^ 0xFFFFFFFFu;
     return t;
 }
 
@@ -1973,8 +1278,7 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t *b = static_cast<const uint8_t *>(d_payloads);
-    // braided fast path; stride <= 16 KiB keeps every per-lane offset (3 strides + frame)
-    // inside the 74 KB table buffer used as the dead-round prefetch target
+    // braided fast path (stride <= 16 KiB: the range the parity tests cover)
     const bool fast = len >= 16 && len <= 1536 && len % 16 == 0 && stride % 16 == 0 && stride <= 16384 &&
                       reinterpret_cast<uintptr_t>(b) % 16 == 0;
     if (fast) return launch_fixed_braid(*s, b, stride, uint32_t(len), n, dev::CrcBEpi{d_out, 0}, st);
@@ -2002,50 +1306,10 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     const uint8_t *b = static_cast<const uint8_t *>(d_base);
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // k_pieces is the path; WTP_VAR_PATH selects the experimental k_mixed / k_var_lane
-    // variants for A/B measurements (both slower on C5).
-    static const int path = [] {
-        const char *e = std::getenv("WTP_VAR_PATH");
-        if (!e) return 1;
-        const char *names[] = {"mixed", "pieces", "lane", "mixed8", "mixed_rb2", "mixed_rb6", "mixed_d4"};
-        for (int i = 0; i < 7; ++i)
-            if (std::strcmp(e, names[i]) == 0) return i;
-        return 0;
-    }();
-    const uint64_t span = (lead + base_bytes + 15) & ~uint64_t(15);
-    if (path != 1 && span >= (1ull << 31))
-        return fail(WTP_EINVAL, "mixed-length view %llu B >= 2 GiB (split the batch)", (unsigned long long)span);
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
-        if (path == 1) {
-            rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
-                               dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
-        } else if (path == 2) {
-            // segments of <= kLnSeg packets, enough of them to cover every CU
-            const uint64_t seg = std::min<uint64_t>(dev::kLnSeg, std::max<uint64_t>(256, (cnt + s->cus - 1) / s->cus));
-            const uint64_t nseg = (cnt + seg - 1) / seg;
-            const unsigned grid = unsigned(std::min<uint64_t>(nseg, uint64_t(s->cus)));
-            hipLaunchKernelGGL(dev::k_var_lane<4>, dim3(grid), dim3(1024), 0, st, b - lead, uint32_t(span), d_offsets + p,
-                               d_lengths + p, uint32_t(lead), cnt, uint32_t(seg), d_out + p, s->tabs, s->status);
-            rc = launch_check("k_var_lane");
-        } else {
-            // 64-packet segments, 16 waves per workgroup, one workgroup per CU (LDS)
-            const uint64_t nseg = (cnt + 63) / 64;
-            const unsigned grid = unsigned(std::min<uint64_t>((nseg + 15) / 16, uint64_t(s->cus)));
-            const uint32_t vspan = uint32_t(base_bytes);
-            auto go = [&](auto kern) {
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, st, b, vspan, d_offsets + p, d_lengths + p, cnt,
-                                   d_out + p, s->tabs, s->status);
-            };
-            switch (path) {  // A/B variants (mixed_d4: ablation, wrong results)
-            case 3: go(dev::k_mixed<8, 4>); break;
-            case 4: go(dev::k_mixed<4, 2>); break;
-            case 5: go(dev::k_mixed<4, 6>); break;
-            case 6: go(dev::k_mixed<4, 4, 4>); break;
-            default: go(dev::k_mixed<4, 4>); break;
-            }
-            rc = launch_check("k_mixed");
-        }
+        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
+                           dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
         if (rc) break;
     }
     return rc;

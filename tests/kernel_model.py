@@ -244,167 +244,3 @@ def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
         p0 = p0n
         rounds += 1
     return out, rounds, hits
-
-
-
-
-def lane_chunks(vo: int, L: int) -> int:
-    """16-B chunks of the (16-B aligned) view a packet touches."""
-    return 0 if L == 0 else ((vo + L + 15) >> 4) - (vo >> 4)
-
-
-def lane_parts(vo: int, L: int):
-    """k_var_lane's tasks for one packet: parts of <= 16 chunks counted back from its last
-    chunk, as (part index j, first chunk address, end address) in the view."""
-    c = lane_chunks(vo, L)
-    m = (c + 15) >> 4
-    e16 = (vo + L + 15) & ~15
-    out = []
-    for j in range(m):
-        ep = e16 - 256 * (m - 1 - j)
-        sp = (vo & ~15) if j == 0 else ep - 256
-        out.append((j, sp, ep))
-    return out
-
-
-class LaneTables:
-    """k_var_lane's tables: 16-B advance word tables (main loop), x^-32, x^-8, the 256-B
-    advance operator (part combine) and shift(~0, m) ^ ~0."""
-
-    def __init__(self):
-        self.a16 = _word_tables(16)
-        self.x32 = _operator(lambda v: O.unshift(v, 4))
-        self.x8 = _operator(lambda v: O.unshift(v, 1))
-        self.a256 = _operator(lambda v: O.shift(v, 256))
-        self.t16 = _operator(lambda v: O.shift(v, 16))
-
-    @staticmethod
-    def sff(m: int) -> int:
-        return O.shift(0xFFFFFFFF, m) ^ 0xFFFFFFFF
-
-
-def var_lane_group(T: LaneTables, view: bytes, tasks):
-    """Phase B of k_var_lane for one group of tasks (vo, L, j, part start, part end): lane
-    i hashes its part over a frame of R = max part chunks rows x 16 B right-aligned at the
-    part's end (rows before the part load as zeros; the packet's head chunk and, in its
-    last part, its last chunk are masked).  4 braids B_k <- A16(B_k) ^ w_k (first row:
-    B_k = w_k); part value P = T16(B0) ^ X(T16(B1) ^ X(T16(B2) ^ X(T16(B3)))), X = x^-32."""
-    R = max((ep - sp) >> 4 for _, _, _, sp, ep in tasks)
-    out = []
-    for vo, L, j, sp, ep in tasks:
-        e = vo + L
-        last = ep >= e
-        B = [0, 0, 0, 0]
-        for t in range(R):
-            a = ep - 16 * (R - t)
-            chunk = bytearray(view[a:a + 16].ljust(16, b"\0")) if a >= sp else bytearray(16)
-            if a == (vo & ~15):
-                for bi in range(vo & 15):
-                    chunk[bi] = 0
-            if t == R - 1 and last:
-                for bi in range(16 - (ep - e), 16):
-                    chunk[bi] = 0
-            w = [int.from_bytes(chunk[4 * k:4 * k + 4], "little") for k in range(4)]
-            B = w if t == 0 else [_apply(T.a16, B[k]) ^ w[k] for k in range(4)]
-        v = _apply(T.t16, B[3])
-        for k in (2, 1, 0):
-            v = _apply(T.t16, B[k]) ^ _apply(T.x32, v)
-        out.append(v)
-    return out
-
-
-def var_lane_combine(T: LaneTables, vo: int, L: int, parts) -> int:
-    """Phase C: Horner over the part values with the 256-B advance, then x^(-8u) for the
-    u bytes after the packet in its last chunk (u>>2 steps of x^-32, u&3 of x^-8)."""
-    acc = parts[0]
-    for p in parts[1:]:
-        acc = _apply(T.a256, acc) ^ p
-    u = ((vo + L + 15) & ~15) - (vo + L)
-    for _ in range(u >> 2):
-        acc = _apply(T.x32, acc)
-    for _ in range(u & 3):
-        acc = _apply(T.x8, acc)
-    return acc ^ T.sff(L)
-
-
-# ---- k_mixed (mixed-length batches): end-aligned frames, forward operators only -------
-# Short packets (<= MX_TH chunks) run one lane per packet over MX_TH 16-B rows aligned so
-# that every lane's packet ends at the end of the last row; long packets run 16 lanes per
-# packet over R rows x 256 B ending at the packet end.  Loads are unaligned 16-B reads at
-# view offset a; a chunk wholly before the packet start reads zeros (out-of-range offset),
-# the straddling chunk masks the bytes before the start, and a chunk at a negative view
-# offset (a packet starting in the view's first 15 bytes) is loaded at offset 0 and moved
-# up by -a bytes.  Every operator is a forward shift: A256, A16 (= shift by 16 B) and
-# S4 (= shift by 4 B, the slice-by-4 word tables).
-MX_TH = 8
-
-
-class MixedTables:
-    def __init__(self):
-        self.a256 = _word_tables(256)
-        self.a16 = _word_tables(16)
-        self.s4 = _word_tables(4)
-
-
-def mx_chunk(view: bytes, a: int, s: int) -> list[int]:
-    """The 4 words a lane hashes for the chunk at view offset a of a packet starting at
-    s: zeros if the chunk ends at or before s; bytes before s masked."""
-    if a + 16 <= s:
-        return [0, 0, 0, 0]
-    if a < 0:
-        raw = b"\0" * (-a) + view[0:16 + a]  # loaded at 0, moved up by -a bytes
-    else:
-        raw = view[a:a + 16]
-    keep = max(s - a, 0)
-    raw = b"\0" * keep + raw[keep:]
-    return [int.from_bytes(raw[4 * k:4 * k + 4], "little") for k in range(4)]
-
-
-def mx_fold(T: MixedTables, b) -> int:
-    """In-lane fold of the 4 braids: S4(S4(S4(b0) ^ b1) ^ b2) ^ b3 (a data word at the
-    frame's last dword)."""
-    v = b[0]
-    for k in range(1, 4):
-        v = _apply(T.s4, v) ^ b[k]
-    return v
-
-
-def mixed_short_crc(T: MixedTables, view: bytes, s: int, L: int) -> int:
-    e = s + L
-    b = [0, 0, 0, 0]
-    for r in range(MX_TH):
-        w = mx_chunk(view, e - 16 * (MX_TH - r), s)
-        b = [_apply(T.a16, b[k]) ^ w[k] for k in range(4)]
-    return _apply(T.s4, mx_fold(T, b)) ^ Tables.init_const(L)
-
-
-def mx_init_xor(w: list[int], rel: int) -> list[int]:
-    """XOR 0xFF into chunk bytes [rel, rel + 4) (the packet's first 4 bytes, rel = s - a):
-    R_{~0}(M) = R_0(M ^ (~0 || 0^(L-4))) for L >= 4, so no init constant is needed."""
-    out = []
-    for d in range(4):
-        lo = min(max(rel - 4 * d, 0), 4)
-        hi = min(max(rel + 4 - 4 * d, 0), 4)
-        m = ((1 << (8 * hi)) - 1) & ~((1 << (8 * lo)) - 1)
-        out.append(w[d] ^ m)
-    return out
-
-
-def mixed_long_crc(T: MixedTables, view: bytes, s: int, L: int, R: int) -> int:
-    """16 lanes over R >= ceil(L/256) rows (L >= 4); the CRC's initial value is XORed
-    into the packet's first 4 bytes as they are loaded; column values v_j combined by
-    Horner with A16 at the flush, then one S4 (the frame's last dword) and ~."""
-    e = s + L
-    fs = e - 256 * R
-    v = []
-    for j in range(G):
-        b = [0, 0, 0, 0]
-        for i in range(R):
-            a = fs + 256 * i + 16 * j
-            w = mx_init_xor(mx_chunk(view, a, s), s - a)
-            b = [_apply(T.a256, b[k]) ^ w[k] for k in range(4)]
-        v.append(mx_fold(T, b))
-    acc = v[0]
-    for j in range(1, G):
-        acc = _apply(T.a16, acc) ^ v[j]
-    return _apply(T.s4, acc) ^ 0xFFFFFFFF

@@ -217,12 +217,11 @@ def test_var_shuffled_offsets_and_empty(W):
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
 
 
-# Mixed-length batches through the product path (WTP_VAR_PATH=lane runs the same cases
-# through the k_var_lane A/B variant): large batches with full 4096-packet segments, lengths around the chunk
-# boundaries, unordered/overlapping offsets, empty payloads, an unaligned base.
+# Mixed-length batches: large batches, lengths around the piece boundaries up to the
+# 4096-B limit, unordered/overlapping offsets, empty payloads, an unaligned base.
 @pytest.mark.parametrize("case", ["uniform_shuffled", "all_long_packed", "all_short", "boundary_lengths", "zipf1.0_lead",
                                   "multi_segment"])
-def test_var_lane_path(W, case):
+def test_var_mixed_cases(W, case):
     rng = np.random.default_rng(11)
     n = {"uniform_shuffled": 100_000, "multi_segment": 1_300_000}.get(case, 70_000)
     lead = 0
@@ -254,9 +253,9 @@ def test_var_lane_path(W, case):
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens)), case
 
 
-# Packets starting in the view's first bytes: k_mixed reads the chunk holding such a
-# start at offset 0 and moves it up (no read before the caller's base); every base
-# alignment, short and long lengths, one packet per lane position.
+# Packets starting in the view's first bytes (their head windows begin before the
+# caller's base, which must read as zeros); every base alignment, short and long
+# lengths, one packet per lane position.
 @pytest.mark.parametrize("lead", [0, 1, 7, 15])
 def test_var_packets_at_view_start(W, lead):
     lens_set = [1, 5, 15, 16, 17, 100, 127, 128, 129, 255, 256, 257, 300, 1456, 4095, 4096]
@@ -277,7 +276,7 @@ def test_var_packets_at_view_start(W, lead):
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens))
 
 
-def test_var_lane_bad_length_sets_status(W):
+def test_var_bad_length_large_batch_sets_status(W):
     W.device_status(0, clear=True)
     n = 70_000
     lens = np.full(n, 700, np.uint32)

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from kernel_model import LaneTables, Tables, braid_crc, lane_parts, pieces_crc, var_lane_combine, var_lane_group
+from kernel_model import Tables, braid_crc, pieces_crc
 
 
 @pytest.fixture(scope="module")
@@ -60,44 +60,3 @@ def test_pieces_rounds_model(T, case):
     assert got == want
     if case in ("packed_zipf", "strided_odd"):
         assert hits == rounds - 1  # every round after the first is prefetched
-
-
-
-
-def test_var_lane_model():
-    """k_var_lane's part split, frame/mask/braid/fold and part combine algebra: lengths up
-    to 4096 B (up to 17 parts), every start alignment, tasks of different sizes in one
-    group."""
-    LT = LaneTables()
-    rng = np.random.default_rng(5)
-    view = O.synth_fill_np(16384, start_byte=77).tobytes()
-    lens = list(range(1, 40)) + [127, 128, 129, 255, 256, 257, 271, 272, 273, 700, 1455, 1456, 1521, 1536, 4095, 4096]
-    for L in lens:
-        pk = [(int(o), L) for o in rng.integers(0, 8192, 4)] + [(o, L) for o in range(16)]
-        pk += [(int(o), int(l)) for o, l in zip(rng.integers(0, 8192, 3), rng.integers(1, L + 1, 3))]
-        tasks = [(vo, l, j, sp, ep) for vo, l in pk for j, sp, ep in lane_parts(vo, l)]
-        assert all(((ep - sp) >> 4) <= 16 for *_, sp, ep in tasks)
-        vals = var_lane_group(LT, view, tasks)
-        k = 0
-        for vo, l in pk:
-            m = len(lane_parts(vo, l))
-            assert var_lane_combine(LT, vo, l, vals[k:k + m]) == O.crc32(view[vo:vo + l]), (vo, l)
-            k += m
-
-
-def test_mixed_model():
-    """k_mixed's algebra: end-aligned frames with forward operators only, the short
-    (lane per packet) and long (16 lanes, R rows) paths, packets at every start offset
-    including the view's first 15 bytes (negative chunk offsets), extra leading rows."""
-    from kernel_model import MX_TH, MixedTables, mixed_long_crc, mixed_short_crc
-    MT = MixedTables()
-    view = O.synth_fill_np(9000, start_byte=5).tobytes()
-    rng = np.random.default_rng(9)
-    for L in [0, 1, 2, 15, 16, 17, 100, 16 * MX_TH]:
-        for s in list(range(0, 18)) + [int(x) for x in rng.integers(0, 8000, 3)]:
-            assert mixed_short_crc(MT, view, s, L) == O.crc32(view[s:s + L]), (s, L)
-    for L in [4, 5, 17, 65, 129, 255, 256, 257, 700, 1456, 4096]:
-        for s in [0, 1, 7, 12, 13, 14, 15, 16, 33] + [int(x) for x in rng.integers(0, 4800, 2)]:
-            R = (L + 255) // 256
-            for extra in (0, 1):
-                assert mixed_long_crc(MT, view, s, L, R + extra) == O.crc32(view[s:s + L]), (s, L, extra)

@@ -2,7 +2,7 @@
 """Where the C5 time goes: the mixed-length kernel timed on length classes of the same
 Zipf batch (same device buffer, compacted offset/length arrays per class).
 
-  python tools/c5_split.py [--s 1.1] [--out f.json]     (WTP_VAR_PATH selects the kernel)
+  python tools/c5_split.py [--s 1.1] [--out f.json]    (WTP_LIB selects an A/B build)
 """
 import argparse
 import json
@@ -60,7 +60,7 @@ def main():
         res.append(r)
     if a.out:
         with open(a.out, "w") as fh:
-            json.dump({"path": os.environ.get("WTP_VAR_PATH", "pieces"), "s": a.s, "results": res}, fh, indent=1)
+            json.dump({"lib": os.environ.get("WTP_LIB", "product"), "s": a.s, "results": res}, fh, indent=1)
 
 
 if __name__ == "__main__":

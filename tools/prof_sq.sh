@@ -1,13 +1,14 @@
 #!/usr/bin/env bash
 # SQ counter passes (one rocprofv3 --pmc run each, kernel trace only) over the C5 /
-# verify driver (tools/prof_pieces.py) for each WTP_VAR_PATH given; output under
+# verify driver (tools/prof_pieces.py) for each library given (WTP_LIB A/B builds, or
+# 'product'); output under
 # gpurun_out/<tag>/<path>/.      usage: tools/prof_sq.sh <tag> <path>...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT="$(pwd)"; TAG="${1:-sq}"; shift; export TMPDIR=/tmp
 for P in "$@"; do
   OUT="$ROOT/gpurun_out/$TAG/$P"; mkdir -p "$OUT"
-  export WTP_VAR_PATH=$P
+  if [ "$P" != product ]; then export WTP_LIB="$ROOT/$P"; else unset WTP_LIB; fi
   i=0
   while read -r counters; do
     [ -z "$counters" ] && continue
