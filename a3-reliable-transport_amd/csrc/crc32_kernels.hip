@@ -576,20 +576,15 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
            (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))))) << 32);
 }
 
-// Pieces of packet p as the main loop counts them (an empty or over-long packet is one).
-template <class Prov>
-__device__ __forceinline__ uint32_t piece_count_of(const Prov &prov, const MetaRaw &r) {
-    uint64_t off;
-    uint32_t len, aux = 0, os = 0;
-    bool ok;
-    prov.decode(r, off, len, ok, aux, os);
+// Pieces of a packet of payload length len as the main loop counts them (an empty or
+// over-long packet is one).  Providers with variable lengths expose load_len(p) (the one
+// metadata word the length comes from) and len_of(word).
+__device__ __forceinline__ uint32_t pieces_of_len(uint32_t len) {
     return (len == 0 || len > kMaxVarLen) ? 1u : (len + kPieceS - 1) / kPieceS;
 }
 template <class Prov>
-__device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p, __amdgpu_buffer_rsrc_t rs) {
-    MetaRaw r{};
-    prov.load(p, r, rs);
-    return piece_count_of(prov, r);
+__device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
+    return pieces_of_len(prov.len_of(prov.load_len(p)));
 }
 
 // Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
@@ -604,32 +599,29 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p, __
 // each, and the target loop had 15 of them).
 struct WaveSplit {
     static constexpr uint32_t kReg = 8, kThreads = 1024, kWaves = kThreads / 64;
-    MetaRaw raw[kReg];
+    uint32_t raw[kReg];  // length words of the first kReg packets of the sub-range
     uint64_t a, b;
     template <class Prov>
-    __device__ __forceinline__ void load(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1) {
+    __device__ __forceinline__ void load(const Prov &prov, uint64_t g0, uint64_t g1) {
         const uint64_t R = g1 - g0;
         a = g0 + ((R * threadIdx.x) >> 10);
         b = g0 + ((R * (threadIdx.x + 1)) >> 10);
         static_assert(kThreads == 1024, "shifts above");
 #pragma unroll
-        for (uint32_t j = 0; j < kReg; ++j) {
-            raw[j] = MetaRaw{};
-            prov.load(a + j < b ? a + j : g0, raw[j], rs);  // g0 < g1: always a valid packet
-        }
+        for (uint32_t j = 0; j < kReg; ++j) raw[j] = prov.load_len(a + j < b ? a + j : g0);  // g0 < g1: valid
     }
     template <class Prov>
-    __device__ __forceinline__ void finish(const Prov &prov, __amdgpu_buffer_rsrc_t rs, uint64_t g0, uint64_t g1,
+    __device__ __forceinline__ void finish(const Prov &prov, uint64_t g0, uint64_t g1,
                                            char *lds, uint32_t wave, uint32_t lane, uint64_t &lo, uint64_t &hi) {
         constexpr uint32_t nw = kWaves;
         const uint64_t m = b - a;
         uint32_t k[kReg], sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) {
-            k[j] = j < m ? piece_count_of(prov, raw[j]) : 0u;
+            k[j] = j < m ? pieces_of_len(prov.len_of(raw[j])) : 0u;
             sum += k[j];
         }
-        for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p, rs);  // > kReg per thread
+        for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p);  // > kReg per thread
         const uint32_t incl = wave_incl_add(sum);
         uint32_t *const wsum = reinterpret_cast<uint32_t *>(lds + kPcBal);
         uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kPcBal + 64);
@@ -658,7 +650,7 @@ struct WaveSplit {
                     pre += step ? k[j] : 0u;
                     p += step ? 1u : 0u;
                 }
-                while (p < b && pre < target) pre += piece_count(prov, p++, rs);
+                while (p < b && pre < target) pre += piece_count(prov, p++);
                 starts[w] = p;
             }
         }
@@ -716,7 +708,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
     PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
     WaveSplit split;
-    if constexpr (Prov::kVarLen) split.load(prov, rs, g0, g1);
+    if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
     PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
     fill_stag(lds, 0, 0, gtab + OFF_S4);
     fill_stag(lds, 0, 1, gtab + OFF_FWD);
@@ -728,7 +720,7 @@ __global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ bas
     }
     uint64_t lo, hi;
     if constexpr (Prov::kVarLen) {
-        split.finish(prov, rs, g0, g1, lds, wave, lane, lo, hi);  // its barriers also publish the tables
+        split.finish(prov, g0, g1, lds, wave, lane, lo, hi);  // its barriers also publish the tables
     } else {
         lo = n * (w0 + wave) / tw;
         hi = n * (w0 + wave + 1) / tw;
@@ -1155,6 +1147,8 @@ struct ArrayProvL {
         r.a = reinterpret_cast<const uint32_t *>(offs)[2 * p];  // low dword: the view is < 2 GiB
         r.b = lens[p];
     }
+    __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
+    __device__ __forceinline__ uint32_t len_of(uint32_t w) const { return w; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
                                            uint32_t &) const {
         off = lead + r.a;
@@ -1181,6 +1175,8 @@ struct DgramProvL {
         r.c = w.x;
         r.d = w.y;
     }
+    __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return rl[p]; }
+    __device__ __forceinline__ uint32_t len_of(uint32_t r) const { return r >= 16 && r <= stride ? r - 16 : 0u; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
                                            uint32_t &) const {
         const uint64_t d = lead + r.a * stride;
