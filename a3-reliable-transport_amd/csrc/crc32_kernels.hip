@@ -590,8 +590,8 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 // Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
 // equal packet counts: with Zipf lengths, equal counts left the busiest wave 1.43x the
 // mean number of rounds (C5, s = 1.1) and the launch waited for it.  Each thread owns a
-// contiguous sub-range; load() issues the metadata loads of its first kReg packets (they
-// fly while the LDS tables fill), finish() sums them, a block scan places the sub-ranges,
+// contiguous sub-range; load() issues the length loads of its first kReg packets (they
+// fly while the LDS tables fill), finish() sums their pieces, a block scan places the sub-ranges,
 // and the thread whose sub-range holds wave w's target (total * w / waves) walks it, from
 // registers, to the first packet at or past the target.  Every thread of the block must
 // call finish() (two barriers).  k_pieces runs 1024-thread blocks: the divisions by the
