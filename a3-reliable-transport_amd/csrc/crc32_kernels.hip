@@ -288,7 +288,10 @@ struct BuildBEpi {
     __device__ __forceinline__ void copy(__amdgpu_buffer_rsrc_t rs, uint32_t q, int32_t rel, bool valid,
                                          u32x4 w) const {
         const uint32_t o = valid ? q * uint32_t(wstride) + 16u + uint32_t(rel) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(w, rs, int(o), 0, 2);  // aux 2: nt (streaming store)
+        // write-back, not nt: a wire slot's rows are 16-B but not 64-B aligned, and L2
+        // merges the segments two rows share (HBM writes 1.11x -> 1.04x of the wire
+        // bytes, 1.2% faster; profiles/r01g/builder_store_ab.txt)
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, int(o), 0, 0);
     }
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
         if (!on) return;
