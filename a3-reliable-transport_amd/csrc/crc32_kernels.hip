@@ -1068,10 +1068,22 @@ int launch_check(const char *what) {
     return WTP_OK;
 }
 
+// Workgroup size of the braided kernel (one workgroup per CU: its LDS tables take the
+// CU's 160 KiB).  Interleaved A/B on one box (profiles/r01i/ab_braid_threads.txt):
+//   CRC / verify, 1 M x 1456 B: 1024 threads 0.2325 ms, 768 0.2334, 640 0.2286,
+//     576 0.2271, 512 0.2219 (86% of HBM peak), 448 0.2289, 384 0.2353, 256 0.2720;
+//   fused builder (reads + wire writes): 1024 0.769 ms, 512 0.745, 256 0.680,
+//     192 0.667, 128 0.653, 64 1.052.
+// Fewer waves per CU keep fewer rows in flight; HBM serves the stream with less
+// queueing (and, for the builder, fewer read/write turnarounds) while 8 resp. 2 waves,
+// two rounds each, still cover its latency.
+constexpr unsigned kBraidThreads = 512;
+constexpr unsigned kBuildThreads = 128;
+
 template <int ROWS, class BEpi>
-void launch_braid_rows(dim3 grid, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len, uint64_t n,
-                       BEpi epi, const uint32_t *tabs) {
-    hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, 0, BEpi>), grid, dim3(1024), 0, st, b,
+void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
+                       uint64_t n, BEpi epi, const uint32_t *tabs) {
+    hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, 0, BEpi>), grid, dim3(threads), 0, st, b,
                        uint32_t(stride), len, n, epi, tabs);
 }
 
@@ -1081,17 +1093,18 @@ template <class BEpi>
 int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
                        hipStream_t st) {
     const int rows = int((len + 255) / 256);
+    const unsigned threads = BEpi::kCopy ? kBuildThreads : kBraidThreads;
     const uint64_t rounds = (n + 3) / 4;
-    const uint64_t want = (rounds + 15) / 16;
+    const uint64_t want = (rounds + threads / 64 - 1) / (threads / 64);
     const unsigned grid = unsigned(want < uint64_t(s.cus) ? want : uint64_t(s.cus));
     epi.cinit = init_const(len);
     switch (rows) {
-        case 1: launch_braid_rows<1>(grid, st, base, stride, len, n, epi, s.tabs); break;
-        case 2: launch_braid_rows<2>(grid, st, base, stride, len, n, epi, s.tabs); break;
-        case 3: launch_braid_rows<3>(grid, st, base, stride, len, n, epi, s.tabs); break;
-        case 4: launch_braid_rows<4>(grid, st, base, stride, len, n, epi, s.tabs); break;
-        case 5: launch_braid_rows<5>(grid, st, base, stride, len, n, epi, s.tabs); break;
-        case 6: launch_braid_rows<6>(grid, st, base, stride, len, n, epi, s.tabs); break;
+        case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 2: launch_braid_rows<2>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 3: launch_braid_rows<3>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 4: launch_braid_rows<4>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 5: launch_braid_rows<5>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 6: launch_braid_rows<6>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
         default: return fail(WTP_EINVAL, "braid rows %d", rows);
     }
     return launch_check("k_fixed_braid");
