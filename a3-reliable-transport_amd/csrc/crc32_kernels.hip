@@ -600,16 +600,20 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 // call finish() (two barriers).  k_pieces runs 1024-thread blocks: the divisions by the
 // thread and wave counts are shifts (64-bit divisions by a runtime value cost ~100 VALU
 // each, and the target loop had 15 of them).
+#ifndef WTP_PC_THREADS
+#define WTP_PC_THREADS 1024
+#endif
+constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThreads);
+static_assert(kPcThreads >= 128 && kPcThreads <= 1024 && (kPcThreads & (kPcThreads - 1)) == 0, "k_pieces block");
 struct WaveSplit {
-    static constexpr uint32_t kReg = 8, kThreads = 1024, kWaves = kThreads / 64;
+    static constexpr uint32_t kReg = 8, kThreads = kPcThreads, kWaves = kThreads / 64;
     uint32_t raw[kReg];  // length words of the first kReg packets of the sub-range
     uint64_t a, b;
     template <class Prov>
     __device__ __forceinline__ void load(const Prov &prov, uint64_t g0, uint64_t g1) {
         const uint64_t R = g1 - g0;
-        a = g0 + ((R * threadIdx.x) >> 10);
-        b = g0 + ((R * (threadIdx.x + 1)) >> 10);
-        static_assert(kThreads == 1024, "shifts above");
+        a = g0 + ((R * threadIdx.x) >> kPcLogT);
+        b = g0 + ((R * (threadIdx.x + 1)) >> kPcLogT);
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) raw[j] = prov.load_len(a + j < b ? a + j : g0);  // g0 < g1: valid
     }
@@ -642,8 +646,7 @@ struct WaveSplit {
         }
         const uint32_t excl = before + incl - sum;
         for (uint32_t w = 1; w < nw; ++w) {
-            const uint32_t target = uint32_t((uint64_t(total) * w) >> 4);
-            static_assert(kWaves == 16, "shift above");
+            const uint32_t target = uint32_t((uint64_t(total) * w) >> (kPcLogT - 6));
             if (target >= excl && target - excl < sum) {
                 uint32_t pre = excl;
                 uint64_t p = a;
@@ -696,7 +699,7 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 // Loads and stores are branch-free (out-of-range buffer offsets for idle lanes), so the
 // prefetches stay in flight across the round.
 template <class Prov, class Epi>
-__global__ __launch_bounds__(1024) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
+__global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
                                                  uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
                                                  uint32_t *__restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
@@ -1121,10 +1124,10 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
     const uint64_t span = (lead + nbytes + 15) & ~uint64_t(15);
     if (span >= (1ull << 31)) return fail(WTP_EINVAL, "general kernel span %llu B >= 2 GiB (split the batch)", (unsigned long long)span);
     const uint64_t waves_want = (n + 63) / 64;
-    uint64_t grid = (waves_want + 15) / 16;
+    uint64_t grid = (waves_want + dev::kPcThreads / 64 - 1) / (dev::kPcThreads / 64);
     if (grid > uint64_t(s.cus)) grid = uint64_t(s.cus);
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(1024), 0, st, b16, uint32_t(span),
+    hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(dev::kPcThreads), 0, st, b16, uint32_t(span),
                        prov, n, epi, s.tabs, s.status);
     return launch_check("k_pieces");
 }
