@@ -336,7 +336,7 @@ struct BuildBEpi {
 // stored once per 8 rounds (on gfx950 stores share vmcnt with loads).
 //
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
-// XOR/shift, bit1 skips the in-lane fold.  Production instantiations use DIAG = 0.
+// XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation.  Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
@@ -485,7 +485,12 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     // copies between the two sets.  (A variant keeping two rounds in flight, with the
     // per-wave invariants hoisted and 8 rounds unrolled, was 0.7-1.3% slower under
     // sustained load, interleaved A/B; it was 7% faster on 64K-packet batches.)
+    // rotating s_setprio per round, offset by the wave's age rank (as in k_pieces): at 8
+    // waves per CU +0.9% sustained (kbench x4, profiles/r01i/kbench_512_prio.log; it lost
+    // 1% at 16 waves).  DIAG bit2 turns it off for ablations.
+    uint32_t prio_round = wave >> 2;
     while (r < rounds) {
+        if (!(DIAG & 4)) rotate_prio(++prio_round);
         load_round(r + rstep, B);
         crc_round(r, A);
         r += rstep;

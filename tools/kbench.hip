@@ -231,7 +231,7 @@ int main(int argc, char **argv) {
     // the product's workgroup size (512 threads, 8 waves per CU) and its ablations
     const unsigned grid512 = unsigned(std::min<uint64_t>((rounds + 7) / 8, s.cus));
 #define BD5(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
-    BD5("braid512_prod", 0); BD5("braid512_nolut", 1); BD5("braid512_nofold", 2); BD5("braid512_skel", 3);
+    BD5("braid512_noprio", 4); BD5("braid512_prod", 0); BD5("braid512_nolut", 1); BD5("braid512_nofold", 2); BD5("braid512_skel", 3);
     vs.push_back({"read_probe_g256x512", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(512), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_nt_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
