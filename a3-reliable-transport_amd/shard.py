@@ -42,20 +42,39 @@ def shard_by_bytes(rank: int, world: int, lengths) -> tuple[int, int]:
     return start(rank), start(rank + 1)
 
 
-def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None, out=None):
-    """Gather every rank's int32 CRC tensor (equal lengths) to `dst`.
+def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None, out=None, n_total: int | None = None):
+    """Gather every rank's int32 CRC tensor to `dst` in packet order.
 
     Returns the concatenated tensor on `dst` (rank order = packet order for the block
     partition) and None elsewhere.  `out` (on `dst`: world * local.numel() elements)
     receives the result in place, with no allocation per call.  With the "nccl"
-    backend this is an RCCL gather over xGMI; with "gloo" it runs on CPU tensors.
+    backend this is an RCCL gather over xGMI.  With "gloo" (CPU tests, or several ranks
+    sharing one GPU) device tensors travel through host memory and the result is a
+    CPU tensor.
+
+    Equal shard sizes are the fast path.  Pass `n_total` (the batch size every rank
+    partitioned with shard_range) and ragged block partitions (n % world != 0) go
+    through gather_crcs_var; without it a shard whose size is not n_total / world is an
+    error rather than a hang inside the collective.
     """
-    import torch
     import torch.distributed as dist
 
     if world == 1:
         return local
+    if n_total is not None:
+        counts = [hi - lo for lo, hi in (shard_range(r, world, n_total) for r in range(world))]
+        if local.numel() != counts[rank]:
+            raise ValueError(f"rank {rank}: local shard has {local.numel()} CRCs, shard_range gives {counts[rank]}")
+        if len(set(counts)) > 1:
+            return gather_crcs_var(local, counts, rank, dst=dst, group=group)
+    if out is not None and rank == dst and out.numel() != world * local.numel():
+        raise ValueError(f"out has {out.numel()} elements, expected {world} x {local.numel()}")
+    on_host = local.is_cuda and dist.get_backend(group) == "gloo"
+    if on_host:
+        local = local.cpu()
+        out = None
     if rank == dst:
+        import torch
         full = out if out is not None else torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
         parts = list(full.view(world, -1).unbind(0))
         dist.gather(local, gather_list=parts, dst=dst, group=group)
@@ -77,6 +96,8 @@ def gather_crcs_var(local, counts, rank: int, dst: int = 0, group=None):
     if world == 1:
         return local
     m = max(counts)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        local = local.cpu()
     padded = torch.zeros(m, dtype=local.dtype, device=local.device)
     padded[:local.numel()] = local
     if rank == dst:

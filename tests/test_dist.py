@@ -2,7 +2,8 @@
 results to rank 0 (a3-reliable-transport_amd/shard.py), world_size 2 and 4 with gloo.
 Each rank checksums its own contiguous shard of the global synthetic stream (the same
 global byte offsets bench.py uses) — here with the CPU oracle, on the GPU box with the
-HIP kernel — and rank 0 compares the gathered vector with the single-process result."""
+HIP kernel (tests/test_gpu_shard.py) — and rank 0 compares the gathered vector with
+the single-process result."""
 import os
 import socket
 
@@ -35,46 +36,70 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_total, q):
+def _worker(rank, world, port, n_total, q, use_gpu=False):
+    """One rank: checksum packets shard_range(rank) of the global synthetic stream (CPU
+    oracle, or the HIP kernel on cuda:0 when use_gpu), then gather to rank 0."""
     import sys
     import torch
     import torch.distributed as dist
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd"), os.path.join(here, "..", "oracle")):
         sys.path.insert(0, p)
-    import oracle as O
     import shard as S
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = S.shard_range(rank, world, n_total)
-    shard_bytes = O.synth_fill_np((hi - lo) * PAYLOAD, start_byte=lo * PAYLOAD)
-    local = O.batch_fixed(shard_bytes, PAYLOAD, PAYLOAD, hi - lo)
-    t = torch.from_numpy(local.view(np.int32).copy())
-    full = S.gather_crcs(t, world, rank)
+    if use_gpu:
+        import wtp_crc32 as W
+        torch.cuda.set_device(0)
+        buf = torch.empty((hi - lo) * PAYLOAD + 16, dtype=torch.uint8, device="cuda")
+        W.synth_fill(buf, start_byte=lo * PAYLOAD, nbytes=(hi - lo) * PAYLOAD)
+        t = torch.empty(hi - lo, dtype=torch.int32, device="cuda")
+        W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, hi - lo, t)
+        torch.cuda.synchronize()
+    else:
+        import oracle as O
+        shard_bytes = O.synth_fill_np((hi - lo) * PAYLOAD, start_byte=lo * PAYLOAD)
+        local = O.batch_fixed(shard_bytes, PAYLOAD, PAYLOAD, hi - lo)
+        t = torch.from_numpy(local.view(np.int32).copy())
+    full = S.gather_crcs(t, world, rank, n_total=n_total)
     if rank == 0:
-        q.put(full.numpy().view(np.uint32).copy())
+        q.put(full.cpu().numpy().view(np.uint32).copy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_gather_matches_single_process(world):
+def run_ranks(world, n_total, use_gpu=False):
+    """Spawn `world` ranks (gloo), return rank 0's gathered vector."""
     import torch.multiprocessing as mp
-    n_total = 512 * world  # equal shards (gather of equal-length tensors)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q, use_gpu)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got = q.get(timeout=180)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 1024), (4, 2048), (3, 1001), (4, 4099)])
+def test_gather_matches_single_process(world, n_total):
+    """Equal shards (fast gather) and ragged block partitions (n % world != 0: padded
+    gather through gather_crcs_var) both return the single-process vector."""
+    got = run_ranks(world, n_total)
     import oracle as O
     want = O.batch_fixed(O.synth_fill_np(n_total * PAYLOAD), PAYLOAD, PAYLOAD, n_total)
     assert np.array_equal(got, want)
+
+
+def test_gather_rejects_wrong_shard_size():
+    import torch
+    with pytest.raises(ValueError):
+        shard.gather_crcs(torch.zeros(5, dtype=torch.int32), 2, 0, n_total=12)
 
 
 def test_shard_by_bytes_balanced():

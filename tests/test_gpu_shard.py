@@ -1,0 +1,108 @@
+"""Multi-GPU path on the GPU box, through the HIP kernel.
+
+- Two / three gloo ranks share the one GPU: each runs wtp_crc32_batch_fixed on its
+  block shard of the global synthetic stream and shard.gather_crcs collects the u32
+  results on rank 0 (equal and ragged partitions), compared element-wise with the
+  oracle.
+- One full C4 per-rank shard (2,097,152 x 1456 B = 3.05 GB, the first > 2 GB braided
+  launch) synthesised at rank 7's global byte offset, element-wise vs the oracle.
+- The RCCL gather itself (nccl backend) on a one-rank group over the HIP results.
+
+Packets are independent (crc32 keeps no state across calls, Crc32.hpp:92-96), so a
+block partition is exact.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+PAYLOAD = 1456
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def W():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import wtp_crc32 as W
+    assert W.LIB.wtp_init(0) == 0, W.LIB.wtp_last_error()
+    return W
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 65536), (3, 100_003)])
+def test_ranks_share_gpu_hip_shards_gather(W, world, n_total):
+    from test_dist import run_ranks
+    got = run_ranks(world, n_total, use_gpu=True)
+    want = O.batch_fixed(O.synth_fill_np(n_total * PAYLOAD), PAYLOAD, PAYLOAD, n_total, threads=THREADS)
+    bad = np.nonzero(got != want)[0]
+    assert got.size == n_total and bad.size == 0, (bad.size, bad[:5])
+
+
+def test_c4_rank7_shard_3gb_elementwise(W):
+    """Config C4: 16 M packets over 8 GPUs = 2,097,152 per rank.  Rank 7's shard starts
+    at global byte 7 * 2,097,152 * 1456 (21.4 GB into the stream)."""
+    n = 2_097_152
+    start = 7 * n * PAYLOAD
+    nbytes = n * PAYLOAD
+    buf = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf, start_byte=start, nbytes=nbytes)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    host = buf[:nbytes].cpu().numpy()
+    # the device bytes are the generator's bytes at that global offset (three 1 MiB windows)
+    for off in (0, nbytes // 2 - (1 << 19), nbytes - (1 << 20)):
+        assert np.array_equal(host[off:off + (1 << 20)], O.synth_fill_np(1 << 20, start_byte=start + off)), off
+    want = O.batch_fixed(host, PAYLOAD, PAYLOAD, n, threads=THREADS)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad.size, bad[:5])
+    del buf, host
+
+
+def _rccl_worker(port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import wtp_crc32 as W
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    n = 4096
+    buf = torch.empty(n * PAYLOAD, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, t)
+    full = torch.empty(n, dtype=torch.int32, device="cuda")
+    dist.gather(t, gather_list=[full], dst=0)  # RCCL gather (one rank: the collective path, no peer)
+    torch.cuda.synchronize()
+    q.put((dist.get_backend(), full.cpu().numpy().view(np.uint32).copy()))
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_one_rank(W):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    backend, got = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    want = O.batch_fixed(O.synth_fill_np(4096 * PAYLOAD), PAYLOAD, PAYLOAD, 4096)
+    assert np.array_equal(got, want)

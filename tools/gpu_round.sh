@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests -> bench -> rocprofv3 kernel-trace stats.
 # Every GPU step has its own time limit; a crash-type exit (fault, abort, segfault,
 # time limit) ends the script without starting further GPU work.
-#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench prof pmc extra cfg profcfg ab recv smoke
+#   usage: tools/gpu_round.sh [tag] [steps...]   steps: tests bench bench2 bench200 prof pmc transient extra cfg profcfg ab recv smoke
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -32,13 +32,16 @@ nproc > "$OUT/host_cpus.txt"; lscpu 2>/dev/null | grep -m1 "Model name" >> "$OUT
 
 for s in $STEPS; do
   case "$s" in
-    tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf --timeout=600 ;;
-    bench) run bench 400 python bench.py ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread ;;
+    bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;        # the driver's invocation
+    bench2) run bench2 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench200) run bench200 400 python bench.py --no-cpu-baseline ;;
     prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline
+             -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
            cd "$ROOT" ;;
+    transient) run transient 200 python -u tools/transient.py --out "$OUT/transient.json" ;;
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-probe
            cd "$ROOT" ;;
     profcfg) cd /tmp && run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/profcfg" -o cfg -- python3 "$ROOT/tools/bench_configs.py" --only "${CFG_ONLY:-c2,c5,verify}" --out "$OUT/profcfg_configs.json"
