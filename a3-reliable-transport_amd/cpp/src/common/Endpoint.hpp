@@ -67,18 +67,24 @@ class Log {
 // reference's one-call-per-packet crc32().
 class Checksums {
    public:
-    explicit Checksums(const std::string &mode) : gpu_(mode == "gpu") {
+    // gpus: devices the sender spreads its file over (0 = every visible device).
+    explicit Checksums(const std::string &mode, int gpus = 1) : gpu_(mode == "gpu"), gpus_(gpus) {
         if (mode != "gpu" && mode != "cpu") throw std::runtime_error("--crc must be cpu or gpu");
         if (gpu_ && wtp_init(0) != WTP_OK) throw std::runtime_error(std::string("GPU CRC unavailable: ") + wtp_last_error());
     }
     bool gpu() const { return gpu_; }
 
-    // Sender build: crc of every kMaxPayload chunk of the file (Sender.cpp:88-92).
+    // Sender build: crc of every kMaxPayload chunk of the file (Sender.cpp:88-92).  With
+    // several GPUs the chunks split into one contiguous range per device (one PCIe link
+    // each); a pinned buffer (wtp_host_alloc) is copied to the devices without staging.
     std::vector<uint32_t> chunks(const uint8_t *buf, size_t n) const {
         const size_t nch = (n + kMaxPayload - 1) / kMaxPayload;
         std::vector<uint32_t> out(nch);
         if (!nch) return out;
-        if (gpu_) {
+        if (gpu_ && gpus_ != 1) {
+            if (wtp_crc32_host_chunked_multi(buf, n, kMaxPayload, out.data(), nullptr, gpus_) != WTP_OK)
+                throw std::runtime_error(std::string("wtp_crc32_host_chunked_multi: ") + wtp_last_error());
+        } else if (gpu_) {
             if (wtp_crc32_host_chunked(buf, n, kMaxPayload, out.data()) != WTP_OK)
                 throw std::runtime_error(std::string("wtp_crc32_host_chunked: ") + wtp_last_error());
         } else {
@@ -87,7 +93,8 @@ class Checksums {
         return out;
     }
 
-    // Receiver verify (Receiver.cpp:203-206): CRC over datagram bytes [16, len).
+    // Receiver verify (Receiver.cpp:203-206): CRC over datagram bytes [16, len).  Only
+    // DATA datagrams are CRC-checked by the reference (Receiver.cpp:139-206).
     bool verify(const uint8_t *dgram, size_t len) const {
         if (len < kHeaderBytes) return false;
         if (gpu_) {
@@ -119,16 +126,20 @@ class Checksums {
 
    private:
     bool gpu_;
+    int gpus_;
 };
 
-// Receive ring for recvmmsg: `slots` datagram slots of kSlot = header + max payload
-// bytes in pinned host memory (wtp_host_alloc), filled by one recvmmsg call per batch.
-// A datagram longer than a slot is truncated by the kernel; its length is then
-// reported as kSlot + 1 so that verify rejects it (the reference reads into a 1500-B
-// buffer and would CRC the truncated bytes; WTP datagrams never exceed 1472 B).
+// Receive ring for recvmmsg: `slots` datagram slots of kSlot = 1504 bytes in pinned host
+// memory (wtp_host_alloc), filled by one recvmmsg call per batch.  Each slot receives
+// into kRecv = 1500 bytes, the reference's `char buffer[1500]` (Receiver.cpp:123-125):
+// a longer datagram is truncated to 1500 bytes exactly as recvfrom truncates it there,
+// and its recv_len is 1500, so verify CRCs the same bytes the reference does.  The slot
+// stride is rounded up to a multiple of 16 so the verify kernel's braided fast path takes
+// the ring (it decides the 1472-B WTP DATA datagrams; other lengths go to its fix-up pass).
 class RecvRing {
    public:
-    static constexpr size_t kSlot = kHeaderBytes + kMaxPayload;  // 1472
+    static constexpr size_t kRecv = 1500;  // Receiver.cpp:123 char buffer[1500]
+    static constexpr size_t kSlot = 1504;  // kRecv rounded up to 16
     // pinned: allocate the ring with wtp_host_alloc (GPU verify: one DMA per batch);
     // otherwise plain page-aligned memory (CPU verify needs no device).
     RecvRing(size_t slots, bool pinned)
@@ -137,7 +148,7 @@ class RecvRing {
           len_(slots), ok_(slots), iov_(slots), msg_(slots), peer_(slots) {
         if (!buf_) throw std::runtime_error("receive ring allocation failed");
         for (size_t i = 0; i < n_; ++i) {
-            iov_[i] = {buf_ + i * kSlot, kSlot};
+            iov_[i] = {buf_ + i * kSlot, kRecv};
             msg_[i].msg_hdr.msg_iov = &iov_[i];
             msg_[i].msg_hdr.msg_iovlen = 1;
         }
@@ -161,10 +172,7 @@ class RecvRing {
         }
         const int got = ::recvmmsg(fd, msg_.data(), unsigned(n_), MSG_WAITFORONE, nullptr);
         if (got <= 0) return 0;
-        for (int i = 0; i < got; ++i) {
-            const bool trunc = (msg_[i].msg_hdr.msg_flags & MSG_TRUNC) != 0;
-            len_[i] = trunc ? uint32_t(kSlot + 1) : uint32_t(msg_[i].msg_len);
-        }
+        for (int i = 0; i < got; ++i) len_[i] = uint32_t(msg_[i].msg_len);  // <= kRecv (truncated like recvfrom)
         return size_t(got);
     }
     uint8_t *slot(size_t i) { return buf_ + i * kSlot; }

@@ -10,9 +10,11 @@
 // packet gets a cumulative ACK carrying the next expected seqNum, START/END are ACKed
 // with their own seqNum, and connection i is stored as <output-dir>/FILE-i.out.
 //
-// Checksum verify follows Receiver.cpp:25-35,203-206: the CRC covers datagram bytes
-// [16, recv_len) — header.length is not trusted — and is compared with the header's
-// checksum; with --crc gpu it runs on the MI355X (wtp_crc32_host_verify).
+// Checksum verify follows Receiver.cpp:25-35,123-125,203-206: datagrams are received into
+// 1500 bytes (longer ones truncated, as recvfrom into char buffer[1500] does), the CRC
+// covers bytes [16, recv_len) — header.length is not trusted — and is compared with the
+// header's checksum, for DATA only (START/END are not checked, Receiver.cpp:139-186);
+// with --crc gpu it runs on the MI355X (wtp_crc32_host_verify).
 // Deliberate differences from the reference: buffered
 // out-of-order packets are flushed in order, the file goes to -d (not the CWD), ACKs
 // are 16-byte datagrams.  --once exits after the first completed connection (tests).
@@ -175,11 +177,13 @@ int main(int argc, char **argv) {
             const size_t got = ring.receive(fd);
             crc.verify_batch(ring.ring(), RecvRing::kSlot, ring.lens(), got, ring.ok());
             for (size_t k = 0; k < got && !done; ++k) {
-                if (!ring.ok()[k]) continue;  // runt, oversize or corrupted: drop, no ACK, no log
                 const uint8_t *buf = ring.slot(k);
                 const size_t n = ring.len(k);
-                const sockaddr_in &peer = ring.peer(k);
+                if (n < kHeaderBytes) continue;  // runt: no header (the reference reads past its end)
                 const PacketHeader h = get_header(buf);
+                // only DATA is CRC-checked, as in the reference (Receiver.cpp:139-206)
+                if (h.type == DATA && !ring.ok()[k]) continue;  // corrupted: drop, no ACK, no log
+                const sockaddr_in &peer = ring.peer(k);
                 log.pkt(h);
 
                 uint32_t ack_seq;

@@ -1,6 +1,6 @@
 // wSender.cpp — WTP sender (go-back-N), config C1 plumbing around the CRC path.
 //
-//   wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu]
+//   wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu] [--gpus N]
 //
 // Reference behaviour (mmheyer/a3-reliable-transport README.md:62-127, cpp/src/base/
 // Sender.cpp): START with a random seqNum until ACKed, DATA seqNums from 0 in chunks of
@@ -8,9 +8,10 @@
 // advance, END with the START seqNum until ACKed.
 //
 // The checksum path is the one this repository accelerates: the whole file is read up
-// front (as Sender.cpp:82 does) and every chunk's CRC is computed in ONE batch — on the
-// MI355X through wtp_crc32_host_chunked with --crc gpu, or with the reference's
-// per-packet crc32() with --crc cpu.  Retransmissions reuse the stored header.
+// front (as Sender.cpp:82 does; into pinned memory with --crc gpu) and every chunk's CRC
+// is computed in ONE batch — on the MI355X through wtp_crc32_host_chunked with --crc gpu
+// (wtp_crc32_host_chunked_multi over N devices with --gpus N, 0 = all), or with the
+// reference's per-packet crc32() with --crc cpu.  Retransmissions reuse the stored header.
 #include <chrono>
 #include <fstream>
 #include <iostream>
@@ -23,6 +24,43 @@ using namespace wtp;
 using Clock = std::chrono::steady_clock;
 
 namespace {
+
+// The input file in one buffer: pinned (wtp_host_alloc) for the GPU path, else heap.
+class InputFile {
+   public:
+    InputFile(const std::string &path, bool pinned) : pinned_(pinned) {
+        std::FILE *f = std::fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("cannot open " + path);
+        std::fseek(f, 0, SEEK_END);
+        const long sz = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        n_ = sz > 0 ? size_t(sz) : 0;
+        p_ = static_cast<uint8_t *>(pinned ? wtp_host_alloc(n_) : std::malloc(n_ ? n_ : 1));
+        const bool ok = p_ && std::fread(p_, 1, n_, f) == n_;
+        std::fclose(f);
+        if (!ok) {
+            release();
+            throw std::runtime_error("cannot read " + path);
+        }
+    }
+    ~InputFile() { release(); }
+    InputFile(const InputFile &) = delete;
+    InputFile &operator=(const InputFile &) = delete;
+    const uint8_t *data() const { return p_; }
+    size_t size() const { return n_; }
+
+   private:
+    void release() {
+        if (pinned_)
+            wtp_host_free(p_);
+        else
+            std::free(p_);
+        p_ = nullptr;
+    }
+    bool pinned_;
+    uint8_t *p_ = nullptr;
+    size_t n_ = 0;
+};
 
 struct Conn {
     int fd;
@@ -67,19 +105,19 @@ int main(int argc, char **argv) {
     try {
         Args a(argc, argv, {{"-h", "host"}, {"--hostname", "host"}, {"-p", "port"}, {"--port", "port"},
                             {"-w", "window"}, {"--window-size", "window"}, {"-i", "input"}, {"--input-file", "input"},
-                            {"-o", "log"}, {"--output-log", "log"}, {"--crc", "crc"}});
+                            {"-o", "log"}, {"--output-log", "log"}, {"--crc", "crc"}, {"--gpus", "gpus"}});
         const int port = std::stoi(a.get("port", "0"));
         const int window = std::stoi(a.get("window", "0"));
         if (port <= 0 || port > 65535 || window <= 0 || !a.has("host") || !a.has("input")) {
-            std::cerr << "usage: wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu]\n";
+            std::cerr << "usage: wSender -h <ip> -p <port> -w <window> -i <input> -o <log> [--crc cpu|gpu] [--gpus N]\n";
             return 1;
         }
-        Checksums crc(a.get("crc", "cpu"));
+        Checksums crc(a.get("crc", "cpu"), std::stoi(a.get("gpus", "1")));
         Log log(a.get("log"));
 
-        std::ifstream in(a.get("input"), std::ios::binary);
-        if (!in) throw std::runtime_error("cannot open " + a.get("input"));
-        std::vector<uint8_t> file((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        // The whole file up front, as Sender.cpp:82 does; with --crc gpu straight into
+        // pinned memory, so the CRC pipeline DMAs it to the device without staging.
+        const InputFile file(a.get("input"), crc.gpu());
 
         // Every DATA checksum in one batch (the device path when --crc gpu).
         const std::vector<uint32_t> sums = crc.chunks(file.data(), file.size());

@@ -230,10 +230,12 @@ struct CrcBEpi {  // out[p] = crc
         if (on) out[p] = v ^ cinit;
     }
 };
-// Receiver verify over a datagram ring with payloads [16, stride): the kernel runs on
-// base = ring + 16, len = stride - 16.  Full datagrams (recv_len == stride) are
-// decided here (Receiver.cpp:203-206: ntohl(header.checksum) == crc32(payload));
-// every other datagram goes to the fix-up list, which the general kernel finishes.
+// Receiver verify over a datagram ring: the kernel runs on base = ring + 16 with the
+// ring's "full" payload length len (1456 for a WTP ring: 1472-B datagrams, whatever the
+// slot stride, e.g. wReceiver's 1504-B slots that hold a 1500-B recvfrom buffer).
+// Datagrams with recv_len == 16 + len are decided here (Receiver.cpp:203-206:
+// ntohl(header.checksum) == crc32(payload)); every other datagram goes to the fix-up
+// list, which the general kernel finishes.
 struct VerifyBEpi {
     static constexpr bool kCopy = false;
     const uint32_t *rl;
@@ -244,6 +246,7 @@ struct VerifyBEpi {
     uint32_t *fix;  // fix[0] = count, fix[1..] = datagram indices
     uint32_t cinit;
     uint64_t n;
+    uint32_t full;  // recv_len of the datagrams this pass decides (16 + len)
     struct Pre {
         uint32_t r, h;
     };
@@ -255,7 +258,7 @@ struct VerifyBEpi {
     }
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &q) const {
         if (!on) return;
-        if (q.r == uint32_t(stride)) {
+        if (q.r == full) {
             const uint32_t c = v ^ cinit;
             ok[p] = bswap32(q.h) == c ? 1 : 0;
             if (crc) crc[p] = c;
@@ -930,9 +933,11 @@ __global__ void k_wire_copy(const uint8_t *__restrict__ src, uint64_t total, uin
         }
     }
 }
-__global__ void k_wire_header(const uint32_t *__restrict__ crc, uint64_t total, uint32_t seq0,
-                              uint8_t *__restrict__ wire, uint64_t wstride, uint32_t *__restrict__ wlen,
-                              uint64_t nchunks) {
+// crc and wlen may be the same buffer (the CRCs are staged in d_wire_len, then become the
+// lengths): neither is __restrict__, so each thread's crc[i] load stays ahead of its
+// wlen[i] store.
+__global__ void k_wire_header(const uint32_t *crc, uint64_t total, uint32_t seq0, uint8_t *__restrict__ wire,
+                              uint64_t wstride, uint32_t *wlen, uint64_t nchunks) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nchunks;
          i += uint64_t(gridDim.x) * blockDim.x) {
         const uint64_t rem = total - i * WTP_MAX_PAYLOAD;
@@ -1031,31 +1036,35 @@ int init_device(int dev) {
         };
         int prev = 0;
         (void)hipGetDevice(&prev);
-        if (hipSetDevice(dev) != hipSuccess) return setfail(WTP_ENODEV, "hipSetDevice failed");
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return setfail(WTP_ENODEV, "hipGetDeviceProperties failed");
-        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-            return setfail(WTP_ENODEV, std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
-        s.cus = prop.multiProcessorCount;
-        std::vector<uint32_t> t = host_tables();
-        if (hipMalloc(&s.tabs, t.size() * 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(tables) failed");
-        if (hipMemcpy(s.tabs, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-            return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
-        if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
-        if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
-        // Scratch of async entry points (verify fix-up list, builder CRCs) comes from a
-        // library-owned pool whose memory is kept across calls (release threshold max):
-        // the default threshold returns it at every synchronisation, and re-mapping it
-        // cost ~1 ms per small host-verify call.
-        hipMemPoolProps pp{};
-        pp.allocType = hipMemAllocationTypePinned;
-        pp.location.type = hipMemLocationTypeDevice;
-        pp.location.id = dev;
-        if (hipMemPoolCreate(&s.pool, &pp) != hipSuccess) return setfail(WTP_EHIP, "hipMemPoolCreate failed");
-        uint64_t keep = UINT64_MAX;
-        if (hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
-            return setfail(WTP_EHIP, "hipMemPoolSetAttribute failed");
-        (void)hipSetDevice(prev);
+        auto setup = [&]() {
+            if (hipSetDevice(dev) != hipSuccess) return setfail(WTP_ENODEV, "hipSetDevice failed");
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return setfail(WTP_ENODEV, "hipGetDeviceProperties failed");
+            if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+                return setfail(WTP_ENODEV, std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
+            s.cus = prop.multiProcessorCount;
+            std::vector<uint32_t> t = host_tables();
+            if (hipMalloc(&s.tabs, t.size() * 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(tables) failed");
+            if (hipMemcpy(s.tabs, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
+            if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
+            if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
+            // Scratch of async entry points (verify fix-up list, builder CRCs) comes from a
+            // library-owned pool whose memory is kept across calls (release threshold max):
+            // the default threshold returns it at every synchronisation, and re-mapping it
+            // cost ~1 ms per small host-verify call.
+            hipMemPoolProps pp{};
+            pp.allocType = hipMemAllocationTypePinned;
+            pp.location.type = hipMemLocationTypeDevice;
+            pp.location.id = dev;
+            if (hipMemPoolCreate(&s.pool, &pp) != hipSuccess) return setfail(WTP_EHIP, "hipMemPoolCreate failed");
+            uint64_t keep = UINT64_MAX;
+            if (hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
+                return setfail(WTP_EHIP, "hipMemPoolSetAttribute failed");
+        };
+        setup();
+        (void)hipSetDevice(prev);  // the caller's current device, on success and on failure
+        (void)hipGetLastError();
     });
     if (s.rc != WTP_OK) return fail(s.rc, "wtp init(device %d): %s", dev, s.err.c_str());
     return WTP_OK;
@@ -1277,11 +1286,15 @@ int wtp_device_status(int device, uint32_t *flags, int clear) {
     int prev = 0;
     WTP_HIP(hipGetDevice(&prev));
     WTP_HIP(hipSetDevice(device));
-    WTP_HIP(hipDeviceSynchronize());
-    WTP_HIP(hipMemcpy(flags, g_dev[device].status, 4, hipMemcpyDeviceToHost));
-    if (clear) WTP_HIP(hipMemset(g_dev[device].status, 0, 4));
-    WTP_HIP(hipSetDevice(prev));
-    return WTP_OK;
+    auto body = [&]() -> int {
+        WTP_HIP(hipDeviceSynchronize());
+        WTP_HIP(hipMemcpy(flags, g_dev[device].status, 4, hipMemcpyDeviceToHost));
+        if (clear) WTP_HIP(hipMemset(g_dev[device].status, 0, 4));
+        return WTP_OK;
+    };
+    rc = body();
+    (void)hipSetDevice(prev);  // restored on failure too
+    return rc;
 }
 
 uint32_t wtp_crc32(const void *buf, size_t size) {
@@ -1345,11 +1358,13 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t *b = static_cast<const uint8_t *>(d_dgrams);
-    // Braided fast path for a 16-B aligned ring whose full datagrams fit one braid frame
-    // (e.g. stride 1472 = header + 1456): it decides every full datagram; the rest
-    // (short, empty or malformed) are listed on the device and the general kernel
-    // finishes them, reading its packet count from the list.
-    if (stride % 16 == 0 && stride >= 32 && stride <= 1552 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
+    // Braided fast path for a 16-B aligned ring: it decides every datagram of the ring's
+    // full WTP length 16 + min(stride - 16, 1456) (1472 B in wReceiver's 1504-B slots or
+    // in a packed 1472-B ring); the rest (short, empty, 1473-1500 B, malformed) are
+    // listed on the device and the general kernel finishes them, reading its packet
+    // count from the list.
+    if (stride % 16 == 0 && stride >= 32 && stride <= 16384 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
+        const uint32_t flen = uint32_t(std::min<size_t>(stride - 16, WTP_MAX_PAYLOAD));
         const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
         uint32_t *fix = nullptr;
         WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&fix), 4 * (std::min<uint64_t>(per, n) + 1), s->pool, st));
@@ -1362,8 +1377,8 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
                 rc = fail(WTP_EHIP, "hipMemsetAsync failed");
                 break;
             }
-            rc = launch_fixed_braid(*s, sb + 16, stride, uint32_t(stride - 16), cnt,
-                                    dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt}, st);
+            rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
+                                    dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt, 16u + flen}, st);
             if (!rc)
                 rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix}, cnt,
                                    dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);

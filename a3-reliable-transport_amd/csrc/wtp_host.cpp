@@ -21,6 +21,8 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "wtp_crc32.h"
 
@@ -115,22 +117,23 @@ extern "C" {
 // Fixed-geometry host batch (also used by wtp_crc32_host_chunked): payload i =
 // h[i*stride, i*stride + len), the last packet may be shorter (tail_len) when
 // `tail_len` != len.
-static int host_fixed_impl(const void *h_payloads, size_t stride, size_t len, size_t n, size_t tail_len,
-                           uint32_t *h_out) {
-    if (n == 0) return WTP_OK;
-    if (!h_payloads || !h_out) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
-    if (len > kSlabBytes || stride > kSlabBytes) return hfail(WTP_EINVAL, "payload/stride larger than a slab", hipSuccess);
-    Pipe *P = nullptr;
-    int rc = pipe_get(P);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(P->mu);
-    const uint8_t *h = static_cast<const uint8_t *>(h_payloads);
-    const bool pinned = is_pinned(h_payloads);
+// Wait for both pipeline streams (errors ignored: the caller is already failing).  Run
+// before any error return from inside a pipelined loop, so no H2D into pin_in / D2H into
+// pin_out of this call is still in flight when the mutex is released and the next caller
+// reuses those buffers (the library keeps no work past its return, wtp_crc32.h).
+static void drain(Pipe *P) {
+    for (int b = 0; b < 2; ++b) (void)hipStreamSynchronize(P->st[b]);
+    (void)hipGetLastError();
+}
+
+static int host_fixed_loop(Pipe *P, const uint8_t *h, bool pinned, size_t stride, size_t len, size_t n,
+                           size_t tail_len, uint32_t *h_out) {
     const size_t step = stride ? stride : 1;
     size_t per = std::min(P->max_pk, std::max<size_t>(1, (kSlabBytes - len) / step + 1));
     if (stride == 0) per = std::min(n, P->max_pk);
     Slab slot[2];
     size_t s = 0;
+    int rc = WTP_OK;
     for (size_t first = 0; first < n || slot[0].live || slot[1].live; ++s) {
         const int b = int(s & 1);
         Slab &sl = slot[b];
@@ -165,6 +168,24 @@ static int host_fixed_impl(const void *h_payloads, size_t stride, size_t len, si
     return WTP_OK;
 }
 
+// Fixed-geometry host batch on the current device (also used by wtp_crc32_host_chunked):
+// payload i = h[i*stride, i*stride + len), the last packet may be shorter (tail_len)
+// when `tail_len` != len.
+static int host_fixed_impl(const void *h_payloads, size_t stride, size_t len, size_t n, size_t tail_len,
+                           uint32_t *h_out) {
+    if (n == 0) return WTP_OK;
+    if (!h_payloads || !h_out) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (len > kSlabBytes || stride > kSlabBytes) return hfail(WTP_EINVAL, "payload/stride larger than a slab", hipSuccess);
+    Pipe *P = nullptr;
+    int rc = pipe_get(P);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(P->mu);
+    rc = host_fixed_loop(P, static_cast<const uint8_t *>(h_payloads), is_pinned(h_payloads), stride, len, n, tail_len,
+                         h_out);
+    if (rc) drain(P);
+    return rc;
+}
+
 int wtp_crc32_host_batch_fixed(const void *h_payloads, size_t stride, size_t len, size_t n, uint32_t *h_out) {
     return host_fixed_impl(h_payloads, stride, len, n, len, h_out);
 }
@@ -177,21 +198,12 @@ int wtp_crc32_host_chunked(const void *h_buf, size_t nbytes, size_t chunk, uint3
     return host_fixed_impl(h_buf, chunk, chunk, n, tail, h_out);
 }
 
-int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len, size_t n, uint8_t *h_ok,
-                          uint32_t *h_crc_out) {
-    if (n == 0) return WTP_OK;
-    if (!h_dgrams || !h_recv_len || !h_ok) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
-    if (stride < 16 || stride > kSlabBytes) return hfail(WTP_EINVAL, "bad datagram stride", hipSuccess);
-    Pipe *P = nullptr;
-    int rc = pipe_get(P);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(P->mu);
-    const uint8_t *h = static_cast<const uint8_t *>(h_dgrams);
-    // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
-    const bool pinned = is_pinned(h_dgrams), lens_pinned = is_pinned(h_recv_len);
+static int host_verify_loop(Pipe *P, const uint8_t *h, bool pinned, size_t stride, const uint32_t *h_recv_len,
+                            bool lens_pinned, size_t n, uint8_t *h_ok, uint32_t *h_crc_out) {
     const size_t per = std::min(P->max_pk, kSlabBytes / stride);
     Slab slot[2];
     size_t s = 0;
+    int rc = WTP_OK;
     for (size_t first = 0; first < n || slot[0].live || slot[1].live; ++s) {
         const int b = int(s & 1);
         Slab &sl = slot[b];
@@ -227,8 +239,70 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     return WTP_OK;
 }
 
-// Pinned host allocation helpers for callers that want zero-copy staging (wSender reads
-// its file straight into such a buffer).
+int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len, size_t n, uint8_t *h_ok,
+                          uint32_t *h_crc_out) {
+    if (n == 0) return WTP_OK;
+    if (!h_dgrams || !h_recv_len || !h_ok) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (stride < 16 || stride > kSlabBytes) return hfail(WTP_EINVAL, "bad datagram stride", hipSuccess);
+    Pipe *P = nullptr;
+    int rc = pipe_get(P);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(P->mu);
+    // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
+    rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), is_pinned(h_dgrams), stride, h_recv_len,
+                          is_pinned(h_recv_len), n, h_ok, h_crc_out);
+    if (rc) drain(P);
+    return rc;
+}
+
+// Multi-GPU host path: the chunks of one host buffer split into ndev contiguous ranges,
+// one pipeline (and one PCIe link, and one CPU staging thread for pageable sources) per
+// device, results written straight into h_out.  Chunks are independent (Crc32.hpp:92-96
+// keeps no state across calls), so no collective is needed: each device's slice of h_out
+// is disjoint.
+int wtp_crc32_host_chunked_multi(const void *h_buf, size_t nbytes, size_t chunk, uint32_t *h_out, const int *devices,
+                                 int ndev) {
+    if (nbytes == 0) return WTP_OK;
+    if (chunk == 0) return hfail(WTP_EINVAL, "chunk == 0", hipSuccess);
+    if (!h_buf || !h_out) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (ndev <= 0) ndev = wtp_device_count();
+    if (ndev <= 0) return hfail(WTP_ENODEV, "no HIP device", hipSuccess);
+    if (ndev > 64) return hfail(WTP_EINVAL, "ndev > 64", hipSuccess);
+    const size_t n = (nbytes + chunk - 1) / chunk;
+    const size_t tail = nbytes - (n - 1) * chunk;
+    const uint8_t *h = static_cast<const uint8_t *>(h_buf);
+    int used = int(std::min<size_t>(size_t(ndev), n));
+    std::vector<int> rcs(used, WTP_OK);
+    std::vector<std::string> msgs(used);
+    auto work = [&](int r) {
+        const int dev = devices ? devices[r] : r;
+        const size_t lo = n * size_t(r) / size_t(used), hi = n * size_t(r + 1) / size_t(used);
+        int prev = 0;
+        int rc = WTP_OK;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(dev) != hipSuccess) {
+            rc = hfail(WTP_ENODEV, "hipSetDevice", hipSuccess);
+        } else {
+            const bool last = hi == n;
+            rc = host_fixed_impl(h + lo * chunk, chunk, chunk, hi - lo, last ? tail : chunk, h_out + lo);
+            (void)hipSetDevice(prev);
+        }
+        rcs[r] = rc;
+        if (rc) msgs[r] = std::string("device ") + std::to_string(dev) + ": " + wtp_last_error();
+    };
+    if (used == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int r = 0; r < used; ++r) th.emplace_back(work, r);
+        for (auto &t : th) t.join();
+    }
+    for (int r = 0; r < used; ++r)
+        if (rcs[r]) return wtp_set_error_(rcs[r], msgs[r].c_str());
+    return WTP_OK;
+}
+
+// Pinned host allocation helpers for callers that want zero-copy staging (wSender --crc
+// gpu reads its file straight into such a buffer; wReceiver's recvmmsg ring lives in one).
 void *wtp_host_alloc(size_t bytes) {
     void *p = nullptr;
     if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;

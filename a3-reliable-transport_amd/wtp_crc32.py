@@ -46,6 +46,7 @@ def _load() -> C.CDLL:
         "wtp_build_data_packets": (i32, [vp, sz, u32, vp, sz, vp, vp]),
         "wtp_crc32_host_batch_fixed": (i32, [vp, sz, sz, sz, vp]),
         "wtp_crc32_host_chunked": (i32, [vp, sz, sz, vp]),
+        "wtp_crc32_host_chunked_multi": (i32, [vp, sz, sz, vp, vp, i32]),
         "wtp_crc32_host_verify": (i32, [vp, sz, vp, sz, vp, vp]),
         "wtp_host_alloc": (vp, [sz]),
         "wtp_host_free": (None, [vp]),
@@ -61,7 +62,7 @@ def _load() -> C.CDLL:
 LIB = _load()
 EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_crc32",
             "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_verify_batch", "wtp_build_data_packets",
-            "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_verify", "wtp_host_alloc",
+            "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify", "wtp_host_alloc",
             "wtp_host_free", "wtp_synth_fill")
 
 
@@ -145,6 +146,19 @@ def host_chunked(buf: np.ndarray, chunk: int = MAX_PAYLOAD, nbytes: int | None =
     nb = buf.nbytes if nbytes is None else nbytes
     out = np.zeros((nb + chunk - 1) // chunk, dtype=np.uint32)
     _check(LIB.wtp_crc32_host_chunked(_np_ptr(buf), nb, chunk, _np_ptr(out)), "host_chunked")
+    return out
+
+
+def host_chunked_multi(buf: np.ndarray, chunk: int = MAX_PAYLOAD, devices=None, nbytes: int | None = None) -> np.ndarray:
+    """host_chunked split over several devices (None: every visible device)."""
+    nb = buf.nbytes if nbytes is None else nbytes
+    out = np.zeros((nb + chunk - 1) // chunk, dtype=np.uint32)
+    if devices is None:
+        dp, nd = None, 0
+    else:
+        dv = (C.c_int * len(devices))(*devices)
+        dp, nd = C.cast(dv, C.c_void_p), len(devices)
+    _check(LIB.wtp_crc32_host_chunked_multi(_np_ptr(buf), nb, chunk, _np_ptr(out), dp, nd), "host_chunked_multi")
     return out
 
 

@@ -103,9 +103,10 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
    above stride (more than the ring slot holds; recvfrom cannot return it) is
    malformed: ok 0.  d_crc_out may be NULL; otherwise it receives the computed CRCs
    (0 for runts and malformed lengths).  Fast path: a 16-B aligned ring with
-   stride % 16 == 0 and stride <= 1552 (e.g. 1472 = header + 1456) runs the braided
-   kernel over every slot's full payload and finishes the datagrams with
-   recv_len != stride in a second, general-kernel pass. */
+   stride % 16 == 0 (e.g. 1472 = header + 1456, or wReceiver's 1504-B slots holding the
+   reference's 1500-B receive buffer) runs the braided kernel over the first
+   min(stride - 16, 1456) payload bytes of every slot, decides the datagrams of exactly
+   that length, and finishes the others in a second, general-kernel pass. */
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len,
                            size_t n, uint8_t *d_ok, uint32_t *d_crc_out, void *stream);
 
@@ -127,6 +128,14 @@ int wtp_crc32_host_batch_fixed(const void *h_payloads, size_t stride, size_t len
    a host buffer (last chunk may be short).  Pipelined: pinned H2D -> CRC -> D2H,
    double-buffered on two HIP streams.  h_out needs ceil(nbytes/chunk) entries. */
 int wtp_crc32_host_chunked(const void *h_buf, size_t nbytes, size_t chunk, uint32_t *h_out);
+
+/* wtp_crc32_host_chunked over several GPUs of this process: the chunks split into ndev
+   contiguous ranges, one pinned pipeline (and PCIe link, and staging thread) per device,
+   results written straight into h_out (chunks are independent, Crc32.hpp:92-96: no
+   collective).  devices = NULL means devices 0 .. ndev-1; ndev <= 0 means every
+   visible device.  The calling thread's current device is unchanged on return. */
+int wtp_crc32_host_chunked_multi(const void *h_buf, size_t nbytes, size_t chunk, uint32_t *h_out,
+                                 const int *devices, int ndev);
 
 /* The wReceiver path, host buffers: same semantics as wtp_crc32_verify_batch. */
 int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len,

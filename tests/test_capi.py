@@ -12,10 +12,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "include", "wtp_crc32.h")
 
 
-def declared_functions():
-    src = open(HDR).read()
+LIBDIR = os.path.join(ROOT, "a3-reliable-transport_amd", "lib")
+# every header under include/ and the library that must export what it declares
+HEADERS = {"wtp_crc32.h": "libwtp_crc32.so", "wtp_diag.h": "libwtp_diag.so", "wtp_group.h": "libwtp_group.so"}
+
+
+def declared_functions(hdr=HDR):
+    src = open(hdr).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(wtp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_header_maps_to_a_library():
+    assert sorted(os.listdir(os.path.join(ROOT, "include"))) == sorted(HEADERS)
+
+
+@pytest.mark.parametrize("hdr,lib", sorted(HEADERS.items()))
+def test_each_library_exports_its_header(hdr, lib):
+    path = os.path.join(LIBDIR, lib)
+    assert os.path.exists(path), f"{lib} not built"
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (wtp_\w+)", out))
+    missing = set(declared_functions(os.path.join(ROOT, "include", hdr))) - exported
+    assert not missing, missing
 
 
 def test_header_declares_the_boundary():

@@ -407,6 +407,45 @@ def test_verify_fast_path(W, n, stride, frac, with_crc):
     assert 0 < want_ok.sum() < n or frac == 1.0 or frac == 0.0
 
 
+def _wtp_ring(n, stride, rng):
+    """wReceiver's ring: 1504-B slots holding up to 1500 received bytes.  Mostly full
+    WTP DATA datagrams (1472 B), some 1473-1500 B (non-WTP senders; the reference CRCs
+    them like any other, Receiver.cpp:123-125,32-33), short ones, runts, corruptions."""
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    rl = np.zeros(n, dtype=np.uint32)
+    body = O.synth_fill_np(n * 1484, start_byte=stride + n)
+    kinds = rng.random(n)
+    for i in range(n):
+        L = 1456 if kinds[i] < 0.75 else (int(rng.integers(1457, 1485)) if kinds[i] < 0.9 else int(rng.integers(0, 1456)))
+        dg = O.build_datagram(i, body[i * 1484:i * 1484 + L].tobytes())
+        buf[i * stride:i * stride + len(dg)] = np.frombuffer(dg, dtype=np.uint8)
+        rl[i] = len(dg)
+    k = n // 40
+    idx = rng.choice(n, 3 * k, replace=False)
+    for i in idx[:k]:
+        buf[i * stride + 16 + int(rng.integers(0, rl[i] - 16 if rl[i] > 16 else 1))] ^= 0x04
+    for i in idx[k:2 * k]:
+        buf[i * stride + 13] ^= 0x01
+    rl[idx[2 * k:]] = rng.integers(0, 16, k).astype(np.uint32)
+    return buf, rl
+
+
+@pytest.mark.parametrize("n", [1, 97, 4099])
+def test_verify_wreceiver_1504_slots(W, n):
+    """1473-1500-B datagrams are verified with the reference's semantics (CRC over
+    [16, recv_len)) at wReceiver's 1504-B stride; full 1472-B WTP datagrams take the
+    braided fast path inside the wider slots."""
+    rng = np.random.default_rng(n)
+    buf, rl = _wtp_ring(n, 1504, rng)
+    assert (rl > 1472).any() or n < 10
+    want_ok, want_crc = O.verify_datagrams(buf, 1504, rl)
+    ok, crc = _verify_dev(W, buf, 1504, rl, n, True)
+    assert np.array_equal(ok, want_ok), np.nonzero(ok != want_ok)[0][:10]
+    assert np.array_equal(crc, want_crc), np.nonzero(crc != want_crc)[0][:10]
+    ok2, crc2 = W.host_verify(buf, 1504, rl)
+    assert np.array_equal(ok2, want_ok) and np.array_equal(crc2, want_crc)
+
+
 def test_verify_misaligned_ring_takes_general_path(W):
     rng = np.random.default_rng(11)
     n, stride = 700, 1472
@@ -572,6 +611,41 @@ def test_c3_1gib_host_chunked_elementwise(W):
     got2 = W.host_chunked(pb.array, 1456)
     pb.free()
     assert np.array_equal(got2, want)
+
+
+@pytest.mark.parametrize("devices", [None, [0], [0, 0, 0]])
+def test_host_chunked_multi(W, devices):
+    """wtp_crc32_host_chunked_multi: chunks split over devices (one pipeline thread per
+    entry; [0, 0, 0] runs three range threads through device 0's pipeline), the last
+    chunk short, vs the oracle element-wise."""
+    nbytes = 200 * (1 << 20) + 777  # > 3 slabs
+    host = O.synth_fill_np(nbytes, start_byte=11)
+    got = W.host_chunked_multi(host, 1456, devices=devices)
+    n = (nbytes + 1455) // 1456
+    want = np.empty(n, np.uint32)
+    want[:-1] = O.batch_fixed(host, 1456, 1456, n - 1, threads=THREADS)
+    want[-1] = O.crc32(host[(n - 1) * 1456:])
+    assert np.array_equal(got, want)
+    dev = torch.cuda.current_device()
+    assert dev == 0  # the caller's device is unchanged
+
+
+def test_host_error_mid_call_then_correct_call(W):
+    """A host wrapper that fails after its first H2D was queued waits for its copies
+    before returning (the next call reuses the same pinned slabs); the next call is
+    exact element-wise."""
+    host = O.synth_fill_np(5000 * 300, start_byte=9)
+    with pytest.raises(W.WtpError):
+        W.host_batch_fixed(host, 5000, 4500, 300)  # len > 4096: fails after the first slab's H2D
+    with pytest.raises(W.WtpError):
+        W.host_chunked_multi(host, 4500, devices=[0, 0])
+    big = O.synth_fill_np(100 * (1 << 20), start_byte=1)
+    got = W.host_chunked(big, 1456)
+    n = got.size
+    want = np.empty(n, np.uint32)
+    want[:-1] = O.batch_fixed(big, 1456, 1456, n - 1, threads=THREADS)
+    want[-1] = O.crc32(big[(n - 1) * 1456:])
+    assert np.array_equal(got, want)
 
 
 def test_host_batch_fixed_odd_stride(W):

@@ -106,3 +106,35 @@ def test_rccl_gather_one_rank(W):
     assert backend == "nccl"
     want = O.batch_fixed(O.synth_fill_np(4096 * PAYLOAD), PAYLOAD, PAYLOAD, 4096)
     assert np.array_equal(got, want)
+
+
+def _group_run(tmp_path, devs, n_per, root):
+    import subprocess
+    import sys
+    out = str(tmp_path / "g.npy")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "group_worker.py"),
+                        out, ",".join(map(str, devs)), ",".join(map(str, n_per)), str(root)],
+                       capture_output=True, text=True, timeout=120)
+    return r, (np.load(out) if r.returncode == 0 else None)
+
+
+@pytest.mark.parametrize("n", [1, 100_003, 1 << 20])
+def test_group_gather_one_device(W, tmp_path, n):
+    """libwtp_group.so (one process, RCCL communicator from ncclCommInitAll): the
+    braided kernel on the shard, then ncclGather of the u32 results to the root."""
+    r, got = _group_run(tmp_path, [0], [n], 0)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = O.batch_fixed(O.synth_fill_np(n * PAYLOAD), PAYLOAD, PAYLOAD, n, threads=THREADS)
+    assert np.array_equal(got, want)
+
+
+def test_group_gather_all_devices(W, tmp_path):
+    """Every visible device one rank, ragged shards (grouped send/recv); on a one-GPU
+    box this is the single-rank ragged-capable path."""
+    nd = torch.cuda.device_count()
+    n_per = [4099 + 7 * r for r in range(nd)]
+    r, got = _group_run(tmp_path, list(range(nd)), n_per, nd - 1)
+    assert r.returncode == 0, r.stdout + r.stderr
+    total = sum(n_per)
+    want = O.batch_fixed(O.synth_fill_np(total * PAYLOAD), PAYLOAD, PAYLOAD, total, threads=THREADS)
+    assert np.array_equal(got, want)

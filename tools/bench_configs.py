@@ -7,7 +7,8 @@
       pageable source (PCIe-bound), plus torch's raw H2D copy rate for reference
   C5  1 M mixed-length payloads, Zipf(s) on [1,1456] (s = 1.1, 1.0), packed, per-packet
       offsets/lengths: the general kernel; read bytes = sum(len) + 12 B metadata/packet
-  verify   1 M wire datagrams (stride 1472) through the receiver-verify kernel
+  verify   1 M wire datagrams (stride 1472, and in wReceiver's 1504-B slots) through the
+           receiver-verify kernel
   build    fused DATA packet builder over a 1.4 GiB payload buffer
 Every line carries a spot parity check against the CPU oracle.
 """
@@ -178,9 +179,22 @@ def verify():
     W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)
     h = wire[:2 * stride].cpu().numpy().tobytes()
     want = O.build_datagram(0, O.synth_fill_np(1456).tobytes()) + b"\0" * 0
+    # wReceiver's ring: the same 1472-B datagrams in 1504-B slots (1500-B receive buffer)
+    del wl
+    w2 = torch.zeros(n * 1504, dtype=torch.uint8, device="cuda")
+    w2.view(n, 1504)[:, :stride].copy_(wire.view(n, stride))
+    rl2 = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    f2 = lambda: W.verify_batch(w2, 1504, rl2, n, ok)  # noqa: E731
+    med2, mean2 = timed(f2, 100)
+    good2 = int(ok.sum().item())
+    del w2, rl2
+    wl = torch.empty(n, dtype=torch.int32, device="cuda")
     return [{"config": "receiver verify, 1M x 1472-B datagrams device-resident", "packets": n,
              "ms_per_launch": round(mean, 4), "payload_GiBps": round(n * 1456 / (mean * 1e-3) / GIB, 1),
              "read_GBps": round(n * (stride + 4) / (mean * 1e-3) / GB, 1), "all_ok": good == n},
+            {"config": "receiver verify, 1M x 1472-B datagrams in 1504-B slots (wReceiver ring)", "packets": n,
+             "ms_per_launch": round(mean2, 4), "payload_GiBps": round(n * 1456 / (mean2 * 1e-3) / GIB, 1),
+             "read_GBps": round(n * (stride + 4) / (mean2 * 1e-3) / GB, 1), "all_ok": good2 == n},
             {"config": "fused DATA packet builder, 1M x 1456 B -> 1472-B wire slots", "packets": n,
              "ms_per_launch": round(bmean, 4), "GBps_read_plus_write": round(n * (1456 + 1472) / (bmean * 1e-3) / GB, 1),
              "d2d_copy_same_bytes_GBps_read_plus_write": round(2 * n * 1456 / (cmean * 1e-3) / GB, 1),
