@@ -58,7 +58,13 @@ constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-
 constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
 constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
 constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
-constexpr uint32_t TAB_WORDS = OFF_HINIT + 68;
+// k_stream (packed mixed lengths): T256 = shift by one 32-B block; 38 nibble operators
+// (8 tables x 16 words each): shift by 128 * 2^k B (k = 0..5, the lane scan), then the
+// payload-length shift in four 3-bit levels (level k, digit j: shift by j * 8^k B).
+constexpr uint32_t OFF_T256 = OFF_HINIT + 68;
+constexpr uint32_t kStNibOps = 6 + 32;
+constexpr uint32_t OFF_NIB = OFF_T256 + 1024;
+constexpr uint32_t TAB_WORDS = OFF_NIB + kStNibOps * 128;
 
 // LDS images (staggered table sets are described at StagKeys below).
 constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
@@ -910,6 +916,325 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
 }
 
 // ------------------------------------------------------------------------------------
+// 2b. stream kernel (packed mixed lengths: payload p+1 starts where payload p ends)
+// ------------------------------------------------------------------------------------
+// A receive buffer or record file holds its payloads back to back, so a wave can hash
+// its region of the byte stream as one uniform stream and read every payload's CRC off
+// prefix values:  P(x) = R_0(stream[X0 .. x)) for the wave's start X0, and
+//   crc(payload [a, b)) = P(b) ^ shift(P(a) ^ ~0, b - a) ^ ~0
+// (R_0(M[a,b)) = P(b) ^ shift(P(a), b - a); the CRC's ~0 init enters as shift(~0, len)).
+// Packed, P(a) of payload p is P(b) of payload p-1.  Per round a wave
+//   1. stages 8 KiB of the stream into its LDS slot (lane-contiguous 1 KiB loads,
+//      prefetched a round ahead); lane l takes bytes [128 l, 128 l + 128);
+//   2. chains its four 32-B blocks independently (slice-by-4, no masking, no rotation:
+//      the stream is 16-B aligned), combines them by Horner with T256 = shift(., 32 B),
+//      scans the 64 lane values with shift(., 128 * 2^k B) seeded with G = P(round
+//      start), and stores the four block anchors P(block start) next to its data;
+//   3. for the payloads that end in this round (lane i <-> payload q + i), evaluates
+//      P(b) = the block anchor fed with the t < 32 bytes of the block before b, takes
+//      P(a) from the lane below (lane 0: the previous payload's), and applies the
+//      length shift in four 3-bit levels of nibble-table operators.
+// Payloads that break the packing (or are >= 4096 B) are found when their metadata is
+// decoded; the wave hands them to a lane-per-payload path at its end (correct for any
+// offsets, slower), so the entry point is exact for every input.
+// Wave ranges inside a workgroup are balanced by bytes + 64 per payload.
+constexpr uint32_t kStThreads = 512, kStWaves = kStThreads / 64;
+constexpr uint32_t kStRound = 8192;                     // stream bytes per wave round
+constexpr uint32_t kStLane = 144;                       // per lane: 128 B of data + 16 B of anchors
+constexpr uint32_t kStSlot = 64 * kStLane;              // 9216 B per wave
+constexpr uint32_t kStNib = 65536;                      // after region 0 (S4 + T256 staggered)
+constexpr uint32_t kStSlots = kStNib + kStNibOps * 512;
+constexpr uint32_t kStBal = kStSlots + kStWaves * kStSlot;
+constexpr uint32_t kStLdsWords = (kStBal + (kStWaves + 1) * 8) / 4;
+constexpr uint32_t kStMaxLen = 4095;  // the length shift has four 3-bit levels
+static_assert(kStLdsWords * 4 <= 163840, "k_stream LDS");
+
+// Operator stored as 8 nibble tables of 16 words at LDS byte address `base` (which may
+// differ per lane): f(v) = XOR_i N_i[(v >> 4i) & 15].  A table's 16 words sit in 16
+// consecutive banks, so a wave-uniform operator never conflicts.
+__device__ __forceinline__ uint32_t nib_apply(const char *lds, uint32_t base, uint32_t v) {
+    uint32_t l[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) l[i] = lds_rd(lds, base + 64u * i + 4u * __builtin_amdgcn_ubfe(v, 4 * i, 4));
+    return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
+}
+
+// P at round position x (0 <= x < kStRound): lane x/128's anchor for the 32-B block
+// holding x, fed with the t = x % 32 block bytes before x (whole words by slice-by-4,
+// then the last r = t % 4 bytes as c' = (c >> 8r) ^ T4((c ^ w) << (32 - 8r))).
+__device__ __forceinline__ uint32_t st_feed(const char *lds, lchar *slot, const StagKeys &K, uint32_t x) {
+    typedef const __attribute__((address_space(3))) uint32_t lu32c;
+    const uint32_t l = x >> 7, blk = (x >> 5) & 3u, t = x & 31u;
+    lchar *const b = slot + l * kStLane + blk * 32u;
+    uint32_t c = *(lu32c *)(slot + l * kStLane + 128u + 4u * blk);
+    const u32x4 w0 = *(const lu32x4 *)b, w1 = *(const lu32x4 *)(b + 16);
+    const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    const uint32_t nw = t >> 2, r = t & 3u;
+    const uint32_t wn = *(lu32c *)(b + 4u * nw);
+#pragma unroll
+    for (uint32_t k = 0; k < 7; ++k) {
+        if (__ballot(k < nw) == 0) break;  // wave-uniform trip count: the largest nw
+        const uint32_t y = stag_apply3<0>(lds, K.kA, K.sel, c ^ w[k]);
+        c = k < nw ? y : c;
+    }
+    const uint32_t y = r ? (c ^ wn) << (32u - 8u * r) : 0u;
+    return (c >> (8u * r)) ^ stag_apply3<0>(lds, K.kA, K.sel, y);
+}
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(kStThreads) void k_stream(const uint8_t *__restrict__ view, uint64_t view_bytes,
+                                                     const uint64_t *__restrict__ offs,
+                                                     const uint32_t *__restrict__ lens, uint64_t lead, uint64_t n,
+                                                     uint32_t *__restrict__ out, const uint32_t *__restrict__ gtab,
+                                                     uint32_t *__restrict__ status) {
+    typedef const __attribute__((address_space(1))) uint64_t gu64;
+    typedef const __attribute__((address_space(1))) uint32_t gu32;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kStLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    const uint64_t g0 = n * blockIdx.x / gridDim.x, g1 = n * (blockIdx.x + 1) / gridDim.x;
+    if (g0 == g1) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto off_of = [&](uint64_t p) { return ((gu64 *)offs)[p] + lead; };  // view offset
+    auto len_of = [&](uint64_t p) { return ((gu32 *)lens)[p]; };
+
+    // --- wave ranges: boundaries at equal weight (bytes + 64 per payload), found among
+    // 512 evenly spaced sample payloads; a prefix max keeps the partition monotone
+    // whatever the offsets hold ------------------------------------------------------
+    uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kStBal);
+    const uint64_t span = g1 - g0;
+    const uint64_t smp = g0 + ((span * threadIdx.x) >> 9);
+    const uint64_t o0 = off_of(g0), oe = off_of(g1 - 1) + len_of(g1 - 1), os = off_of(smp);
+    if (threadIdx.x <= kStWaves) starts[threadIdx.x] = threadIdx.x == 0 ? g0 : g1;
+    fill_stag(lds, 0, 0, gtab + OFF_S4);
+    fill_stag(lds, 0, 1, gtab + OFF_T256);
+    {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kStNib);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_NIB);
+        for (uint32_t i = threadIdx.x; i < kStNibOps * 32; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    {
+        const uint64_t wtot = (oe - o0) + 64 * span, wsm = (os - o0) + 64 * (smp - g0);
+        for (uint32_t w = 1; w < kStWaves; ++w) {
+            const uint64_t m = __ballot(wsm >= (wtot >> 3) * w);
+            if (m && lane == uint32_t(__builtin_ctzll(m))) atomicMin(reinterpret_cast<unsigned long long *>(starts + w),
+                                                                    (unsigned long long)smp);
+        }
+    }
+    __syncthreads();
+    uint64_t lo = starts[0];
+    for (uint32_t w = 1; w <= wave; ++w) lo = starts[w] > lo ? starts[w] : lo;
+    const uint64_t hi = starts[wave + 1] > lo ? starts[wave + 1] : lo;
+    lo = uniform64(lo);
+    if (lo >= hi) return;  // no block barrier below this point
+
+    const StagKeys K(lane);
+    lchar *const slot = (lchar *)lds_w + kStSlots + wave * kStSlot;
+    const uint64_t vabs = uint64_t(reinterpret_cast<uintptr_t>(view));
+    const uint64_t vb16 = (view_bytes + 15) & ~uint64_t(15);
+
+    // --- metadata: groups of 64 payloads; lane i of group gs <-> payload gs + i -------
+    auto load_group = [&](uint64_t gs, uint64_t &o, uint32_t &l) {
+        const uint64_t p = gs + lane, pc = p < hi ? p : hi - 1;
+        o = off_of(pc);
+        l = len_of(pc);
+    };
+    uint64_t oA, oB, oC;
+    uint32_t lA, lB, lC;
+    load_group(lo, oA, lA);
+    load_group(lo + 64, oB, lB);
+    const uint64_t o_lo = uniform64(__builtin_amdgcn_readfirstlane(uint32_t(oA)) |
+                                    (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(oA >> 32))) << 32));
+    const uint64_t wb = ((vabs + o_lo) & ~uint64_t(127)) - vabs;  // X0 (view offset, mod 2^64)
+    uint64_t fb = hi;    // first payload that breaks the packing (wave-uniform)
+    uint64_t pe = o_lo;  // end of the payload before the group being decoded
+    // decode: relative end e (to X0) and length; flags the first payload that is not
+    // packed, is >= 4096 B, or lies outside 4 GiB of X0
+    auto decode = [&](uint64_t gs, uint64_t o, uint32_t l, uint32_t &e, uint32_t &len) {
+        const uint64_t end = o + l;
+        const uint32_t plo = uint32_t(__builtin_amdgcn_update_dpp(int(uint32_t(pe)), int(uint32_t(end)), 0x138, 0xF, 0xF, false));
+        const uint32_t phi = uint32_t(__builtin_amdgcn_update_dpp(int(uint32_t(pe >> 32)), int(uint32_t(end >> 32)), 0x138, 0xF, 0xF, false));
+        const uint64_t prev = uint64_t(plo) | (uint64_t(phi) << 32);  // lane 0: pe (wave_shr:1 keeps old)
+        const uint64_t p = gs + lane;
+        const bool bad = p < hi && ((p > lo && o != prev) || l > kStMaxLen || end - wb >= (1ull << 32));
+        const uint64_t m = __ballot(bad);
+        if (m) {
+            const uint64_t f = gs + uint64_t(__builtin_ctzll(m));
+            fb = f < fb ? f : fb;
+        }
+        e = uint32_t(end - wb);
+        len = l;
+        pe = uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(end)), 63))) |
+             (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(end >> 32)), 63))) << 32);
+    };
+    uint32_t eA, nA, eB, nB;
+    decode(lo, oA, lA, eA, nA);
+    decode(lo + 64, oB, lB, eB, nB);
+
+    // --- stream rounds ------------------------------------------------------------------
+    auto load_round = [&](uint64_t rrel, u32x4 (&x)[8]) {
+        const int64_t st = int64_t(wb + rrel);
+        const uint64_t sp = st < 0 ? 0 : uint64_t(st);
+        const int32_t adj = int32_t(st - int64_t(sp));  // <= 0: chunks before the view read 0
+        const uint64_t left = sp < vb16 ? vb16 - sp : 0;
+        const auto rs = make_rsrc(view + sp, uint32_t(left < 0x7FFFFFF0u ? left : 0x7FFFFFF0u));
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rs, int(uint32_t(adj) + 16u * (64u * i + lane)), 0, 2));
+    };
+    u32x4 x[8];
+    load_round(0, x);
+    uint64_t rrel = 0, gsA = lo;
+    uint32_t G = 0, d = 0, cP = 0;
+    bool first = true;
+    const uint32_t scan0 = kStNib;  // shift by 128 B
+    for (;;) {
+        // 1. stage (chunk c of the round -> lane c/8's data at 16 (c % 8)) and prefetch
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t c = 64u * i + lane;
+            *(lu32x4 *)(slot + kStLane * (c >> 3) + 16u * (c & 7u)) = x[i];
+        }
+        // group C (the one after B) is (re)issued before the prefetch, so a rotation in
+        // this round waits for it with a counted vmcnt that leaves the prefetch in flight
+        load_group(gsA + 128, oC, lC);
+        load_round(rrel + kStRound, x);
+        bool rotated = false;
+        __builtin_amdgcn_wave_barrier();
+        // 2. chain the lane's four 32-B blocks (independent), Horner, scan, anchors
+        uint32_t w[32];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const u32x4 y = *(const lu32x4 *)(slot + kStLane * lane + 16u * u);
+            w[4 * u] = y.x;
+            w[4 * u + 1] = y.y;
+            w[4 * u + 2] = y.z;
+            w[4 * u + 3] = y.w;
+        }
+        uint32_t cb[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) cb[j] = w[8 * j];
+#pragma unroll
+        for (uint32_t k = 1; k < 8; ++k)
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) cb[j] = stag_apply3x<0>(lds, K.kA, K.sel, cb[j], w[8 * j + k]);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) cb[j] = stag_apply3<0>(lds, K.kA, K.sel, cb[j]);  // R_0(block j)
+        uint32_t V = cb[0];
+#pragma unroll
+        for (uint32_t j = 1; j < 4; ++j) V = stag_apply3x<128>(lds, K.kA, K.sel, V, cb[j]);  // T256(V) ^ c_j
+        const uint32_t gs128 = nib_apply(lds, scan0, G);  // shift(G, 128 B)
+        uint32_t I = V ^ (lane == 0 ? gs128 : 0u);
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) {
+            const uint32_t dd = 1u << k;
+            const uint32_t y = nib_apply(lds, kStNib + 512u * k, __shfl_up(I, dd));
+            I = lane >= dd ? I ^ y : I;
+        }
+        uint32_t A0 = __shfl_up(I, 1);
+        A0 = lane == 0 ? G : A0;
+        const uint32_t A1 = stag_apply3x<128>(lds, K.kA, K.sel, A0, cb[0]);
+        const uint32_t A2 = stag_apply3x<128>(lds, K.kA, K.sel, A1, cb[1]);
+        const uint32_t A3 = stag_apply3x<128>(lds, K.kA, K.sel, A2, cb[2]);
+        *(lu32x4 *)(slot + kStLane * lane + 128u) = u32x4{A0, A1, A2, A3};
+        const uint32_t Gn = __builtin_amdgcn_readlane(I, 63);
+        __builtin_amdgcn_wave_barrier();
+        if (first) {  // P(a) of the wave's first payload
+            cP = __builtin_amdgcn_readfirstlane(st_feed(lds, slot, K, uint32_t(o_lo - wb)));
+            first = false;
+        }
+        // 3. the payloads that end in this round, 64 at a time (fb can drop when a group
+        // is decoded at a rotation, so the end of the fast range is re-read each time)
+        for (;;) {
+            const uint64_t pend = fb < hi ? fb : hi;
+            const uint32_t idx = d + lane;
+            const uint32_t src = (idx & 63u) << 2;
+            const uint32_t ea = uint32_t(__builtin_amdgcn_ds_bpermute(int(src), int(eA)));
+            const uint32_t eb = uint32_t(__builtin_amdgcn_ds_bpermute(int(src), int(eB)));
+            const uint32_t na = uint32_t(__builtin_amdgcn_ds_bpermute(int(src), int(nA)));
+            const uint32_t nb = uint32_t(__builtin_amdgcn_ds_bpermute(int(src), int(nB)));
+            const uint32_t e = idx < 64u ? ea : eb, len = idx < 64u ? na : nb;
+            const uint64_t p = gsA + idx;
+            const bool ends = p < pend && uint64_t(e) < rrel + kStRound;
+            const uint64_t em = __ballot(ends);
+            if (em == 0) break;
+            const uint32_t m = uint32_t(__popcll(em));  // a prefix of the lanes: ends are sorted
+            const uint32_t pb = st_feed(lds, slot, K, ends ? uint32_t(e - uint32_t(rrel)) : 0u);
+            uint32_t v = __shfl_up(pb, 1);
+            v = (lane == 0 ? cP : v) ^ 0xFFFFFFFFu;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) v = nib_apply(lds, kStNib + 512u * (6u + 8u * k + ((len >> (3 * k)) & 7u)), v);
+            const auto ro = make_rsrc(out + gsA + d, 256u);
+            __builtin_amdgcn_raw_buffer_store_b32(pb ^ v ^ 0xFFFFFFFFu, ro, ends ? int(4u * lane) : int(0x80000000u), 0, 0);
+            cP = __builtin_amdgcn_readlane(pb, m - 1);
+            d += m;
+            if (d >= 64u) {  // group A done: B -> A, C -> B
+                eA = eB;
+                nA = nB;
+                gsA += 64;
+                d -= 64u;
+                if (rotated) {  // a second rotation this round (> ~128 short payloads): load C now
+                    load_group(gsA + 64, oC, lC);
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                }
+                decode(gsA + 64, oC, lC, eB, nB);
+                rotated = true;
+            }
+            if (m < 64u) break;
+        }
+        if (gsA + d >= (fb < hi ? fb : hi)) break;
+        G = Gn;
+        rrel += kStRound;
+    }
+
+    // --- payloads [fb, hi): one lane per payload, 16-B chunks straight from memory
+    // (the next chunk prefetched while this one is fed word by word) --------------------
+    typedef const __attribute__((address_space(1))) u32x4 gq;
+    for (uint64_t g = fb; g < hi; g += 64) {
+        const uint64_t p = g + lane, pc = p < hi ? p : hi - 1;
+        const uint64_t o = off_of(pc);
+        const uint32_t l0 = len_of(pc);
+        const bool have = p < hi, over = l0 > kMaxVarLen;
+        if (have && over) atomicOr(status, 1u);
+        const int32_t L = have && !over ? int32_t(l0) : 0;
+        const uint64_t a0 = o & ~uint64_t(15);
+        const int32_t ld0 = int32_t(o & 15u);
+        const uint32_t nq = L ? uint32_t(ld0 + L + 15) >> 4 : 0u;
+        auto chunk = [&](uint32_t k) {  // chunk k of the payload, 0 outside the view
+            const uint64_t a = a0 + 16ull * k;
+            const bool in = k < nq && a + 16 <= vb16;
+            gq *const src = in ? (gq *)view + (a >> 4) : (gq *)gtab;  // never an address outside the view
+            const u32x4 q = *src;
+            return in ? q : u32x4{0u, 0u, 0u, 0u};
+        };
+        uint32_t c = 0xFFFFFFFFu;
+        u32x4 cur = chunk(0);
+        for (uint32_t k = 0;; ++k) {
+            if (__ballot(k < nq) == 0) break;
+            const u32x4 nxt = chunk(k + 1);
+            const uint32_t wv[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                // payload bytes [b0, b0 + 4) of this word; feed its bytes in [0, L)
+                const int32_t b0 = int32_t(16u * k + 4u * u) - ld0;
+                const int32_t s0 = b0 < 0 ? -b0 : 0, e0 = L - b0 < 4 ? L - b0 : 4;
+                const int32_t r = e0 - s0;
+                const uint32_t rr = r > 0 ? uint32_t(r) : 4u, ss = s0 < 4 ? uint32_t(s0) : 0u;
+                const uint32_t yv = wv[u] >> (8u * ss);
+                const uint32_t c2 = uint32_t(uint64_t(c) >> (8u * rr)) ^
+                                    stag_apply3<0>(lds, K.kA, K.sel, uint32_t(uint64_t(c ^ yv) << (32u - 8u * rr)));
+                c = r > 0 && k < nq ? c2 : c;
+            }
+            cur = nxt;
+        }
+        const auto ro = make_rsrc(out + g, 256u);
+        __builtin_amdgcn_raw_buffer_store_b32(c ^ 0xFFFFFFFFu, ro, have ? int(4u * lane) : int(0x80000000u), 0, 0);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // 3. fused DATA packet builder
 // ------------------------------------------------------------------------------------
 // Stage A: copy chunk i into its wire slot after a 16-B header hole; CRC computed on
@@ -1023,6 +1348,14 @@ std::vector<uint32_t> host_tables() {
         make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
     }
     for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
+    make_operator(&t[OFF_T256], [](uint32_t v) { return shift_bytes(v, 32); });
+    auto nib = [&](uint32_t op, uint64_t nbytes) {
+        for (uint32_t i = 0; i < 8; ++i)
+            for (uint32_t e = 0; e < 16; ++e) t[OFF_NIB + 128 * op + 16 * i + e] = shift_bytes(e << (4 * i), nbytes);
+    };
+    for (uint32_t k = 0; k < 6; ++k) nib(k, uint64_t(128) << k);
+    for (uint32_t k = 0; k < 4; ++k)
+        for (uint32_t j = 0; j < 8; ++j) nib(6 + 8 * k + j, uint64_t(j) << (3 * k));
     return t;
 }
 
@@ -1144,6 +1477,19 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
     hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(dev::kPcThreads), 0, st, b16, uint32_t(span),
                        prov, n, epi, s.tabs, s.status);
     return launch_check("k_pieces");
+}
+
+// Packed mixed lengths (k_stream): one launch for any n and any buffer size (64-bit
+// offsets, per-round buffer resources); the kernel finds its own workgroup ranges.
+int launch_stream(DevState &s, const uint8_t *base, uint64_t nbytes, const uint64_t *offs, const uint32_t *lens,
+                  uint64_t n, uint32_t *out, hipStream_t st) {
+    const uint64_t lead = reinterpret_cast<uintptr_t>(base) & 15u;
+    uint64_t grid = (n + dev::kStWaves * 64 - 1) / (dev::kStWaves * 64);  // >= 64 payloads per wave
+    if (grid > uint64_t(s.cus)) grid = uint64_t(s.cus);
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((dev::k_stream<0>), dim3(unsigned(grid)), dim3(dev::kStThreads), 0, st, base - lead,
+                       lead + nbytes, offs, lens, lead, n, out, s.tabs, s.status);
+    return launch_check("k_stream");
 }
 
 }  // namespace
@@ -1346,6 +1692,17 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
         if (rc) break;
     }
     return rc;
+}
+
+int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
+                           const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream) {
+    if (n == 0) return WTP_OK;
+    if (!d_base || !d_offsets || !d_lengths || !d_out) return fail(WTP_EINVAL, "null pointer");
+    DevState *s = nullptr;
+    int rc = current(s);
+    if (rc) return rc;
+    return launch_stream(*s, static_cast<const uint8_t *>(d_base), base_bytes, d_offsets, d_lengths, n, d_out,
+                         static_cast<hipStream_t>(stream));
 }
 
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len, size_t n,

@@ -42,6 +42,7 @@ def _load() -> C.CDLL:
         "wtp_crc32": (u32, [vp, sz]),
         "wtp_crc32_batch_fixed": (i32, [vp, sz, sz, sz, vp, vp]),
         "wtp_crc32_batch_var": (i32, [vp, sz, vp, vp, sz, vp, vp]),
+        "wtp_crc32_batch_packed": (i32, [vp, sz, vp, vp, sz, vp, vp]),
         "wtp_crc32_verify_batch": (i32, [vp, sz, vp, sz, vp, vp, vp]),
         "wtp_build_data_packets": (i32, [vp, sz, u32, vp, sz, vp, vp]),
         "wtp_crc32_host_batch_fixed": (i32, [vp, sz, sz, sz, vp]),
@@ -61,7 +62,7 @@ def _load() -> C.CDLL:
 
 LIB = _load()
 EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_crc32",
-            "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_verify_batch", "wtp_build_data_packets",
+            "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_batch_packed", "wtp_crc32_verify_batch", "wtp_build_data_packets",
             "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify", "wtp_host_alloc",
             "wtp_host_free", "wtp_synth_fill")
 
@@ -107,6 +108,12 @@ def crc32_batch_fixed(payloads, stride: int, length: int, n: int, out, stream=No
 def crc32_batch_var(base, base_bytes: int, offsets, lengths, n: int, out, stream=None) -> None:
     _check(LIB.wtp_crc32_batch_var(_dptr(base), base_bytes, _dptr(offsets), _dptr(lengths), n, _dptr(out),
                                    _stream(stream)), "wtp_crc32_batch_var")
+
+
+def crc32_batch_packed(base, base_bytes: int, offsets, lengths, n: int, out, stream=None) -> None:
+    """Back-to-back payloads (offsets = exclusive prefix sum of lengths): k_stream."""
+    _check(LIB.wtp_crc32_batch_packed(_dptr(base), base_bytes, _dptr(offsets), _dptr(lengths), n, _dptr(out),
+                                      _stream(stream)), "wtp_crc32_batch_packed")
 
 
 def verify_batch(dgrams, stride: int, recv_len, n: int, ok, crc_out=None, stream=None) -> None:

@@ -95,6 +95,17 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
 int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                         const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
+/* Mixed lengths stored back to back (a receive buffer, a record file): as
+   wtp_crc32_batch_var with d_offsets[i+1] == d_offsets[i] + d_lengths[i] (offsets =
+   exclusive prefix sum of the lengths, any first offset).  Each wave hashes its region
+   of the byte stream once and reads every payload's CRC off prefix values (no per-
+   payload windows, masks or padding).  No limit on base_bytes (64-bit offsets) or n.
+   Payloads that break the packing, or are longer than 4095 B, are still computed
+   exactly on a slower lane-per-payload path, so results are correct for any offsets;
+   lengths > WTP_MAX_KERNEL_LEN give crc 0 and set the status flag. */
+int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
+                           const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
+
 /* Receiver verify, batched (cpp/src/base/Receiver.cpp:25-35 + :203-206): datagram i is
    d_dgrams[i*stride .. i*stride + d_recv_len[i]) = 16-B big-endian PacketHeader ||
    payload.  As in the reference, the CRC covers bytes [16, recv_len) and

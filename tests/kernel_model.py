@@ -244,3 +244,122 @@ def pieces_rounds(T: Tables, buf: bytes, offs, lens, rng=None):
         p0 = p0n
         rounds += 1
     return out, rounds, hits
+
+
+# ---- k_stream: packed mixed-length payloads (payload p+1 starts where p ends) --------
+ST_ROUND = 8192  # bytes per wave round: 64 lanes x 128 B
+ST_LANE = 128
+ST_BLK = 32
+
+
+def nib_tables(f) -> np.ndarray:
+    """A linear operator as 8 nibble tables of 16 words: N[i][e] = f(e << 4i)."""
+    out = np.zeros((8, 16), dtype=np.uint32)
+    for i in range(8):
+        for e in range(16):
+            out[i, e] = f(e << (4 * i))
+    return out
+
+
+def nib_apply(N: np.ndarray, v: int) -> int:
+    r = 0
+    for i in range(8):
+        r ^= int(N[i, (v >> (4 * i)) & 15])
+    return r
+
+
+class StreamTables:
+    """Tables of k_stream: slice-by-4 (advance 4 B), T256 (shift by one 32-B block),
+    scan operators shift by 128 * 2^k B (k = 0..5), and the length shift in four
+    3-bit levels: level k, digit j -> shift by j * 8^k bytes (lengths < 4096)."""
+
+    def __init__(self):
+        self.s4 = _word_tables(4)
+        self.t256 = _operator(lambda v: O.shift(v, ST_BLK))
+        self.scan = [nib_tables(lambda v, k=k: O.shift(v, ST_LANE << k)) for k in range(6)]
+        self.lenop = [[nib_tables(lambda v, n=j * 8 ** k: O.shift(v, n)) for j in range(8)] for k in range(4)]
+
+    def shift_len(self, v: int, L: int) -> int:
+        for k in range(4):
+            v = nib_apply(self.lenop[k][(L >> (3 * k)) & 7], v)
+        return v
+
+
+def stream_wave(T: StreamTables, buf: bytes, offs, lens, view_addr: int = 0):
+    """One wave of k_stream over packed packets (offs[i+1] == offs[i] + lens[i]) of the
+    view `buf` (loads outside it read 0).  Mirrors csrc/crc32_kernels.hip: 8 KiB rounds
+    staged lane-contiguously, lane l chains its 128 B as four 32-B blocks (slice-by-4,
+    no masking), Horner over the blocks with T256, an inclusive scan over the 64 lanes
+    seeded with the round anchor G = P(R), block anchors A = P(block start); per packet
+    P(b) = A fed with the t < 32 bytes of its block before b, and
+    crc = P(b) ^ shift(P(a) ^ ~0, len) ^ ~0 with P(a) = the previous packet's P(b).
+    P(x) = R_0(view[R0 .. x)) for the wave's first round start R0.  Returns (crcs, rounds)."""
+    n = len(lens)
+    nb = len(buf)
+
+    def rd16(o):  # the host rounds the view up to 16 B: a chunk holding a valid byte is in range
+        return bytes(16) if o < 0 or o >= nb else bytes(buf[o:o + 16]).ljust(16, b"\0")
+
+    def le(b, i):
+        return int.from_bytes(b[i:i + 4], "little")
+
+    a_lo = int(offs[0])
+    R = ((view_addr + a_lo) & ~127) - view_addr
+    G = 0
+    out = [None] * n
+    cur = 0
+    cP = None
+    rounds = 0
+    while cur < n:
+        data = b"".join(rd16(R + 16 * c) for c in range(ST_ROUND // 16))
+        C, V = [], []
+        for l in range(64):
+            seg = data[ST_LANE * l:ST_LANE * (l + 1)]
+            cs = []
+            for j in range(4):
+                c = le(seg, ST_BLK * j)
+                for k in range(1, 8):
+                    c = _apply(T.s4, c) ^ le(seg, ST_BLK * j + 4 * k)
+                cs.append(_apply(T.s4, c))
+            H = cs[0]
+            for j in range(1, 4):
+                H = _apply(T.t256, H) ^ cs[j]
+            C.append(cs)
+            V.append(H)
+        I = list(V)
+        I[0] ^= nib_apply(T.scan[0], G)
+        for k in range(6):
+            d = 1 << k
+            I = [I[l] ^ nib_apply(T.scan[k], I[l - d]) if l >= d else I[l] for l in range(64)]
+        E = [G] + I[:63]
+        A = []
+        for l in range(64):
+            a = [E[l]]
+            for j in range(3):
+                a.append(_apply(T.t256, a[-1]) ^ C[l][j])
+            A.append(a)
+
+        def P(x):
+            assert 0 <= x < ST_ROUND
+            l, blk, t = x >> 7, (x >> 5) & 3, x & 31
+            c = A[l][blk]
+            base = ST_LANE * l + ST_BLK * blk
+            for k in range(t >> 2):
+                c = _apply(T.s4, c ^ le(data, base + 4 * k))
+            r = t & 3
+            if r:
+                y = ((c ^ le(data, base + 4 * (t >> 2))) << (8 * (4 - r))) & 0xFFFFFFFF
+                c = (c >> (8 * r)) ^ _apply(T.s4, y)
+            return c
+
+        if cP is None:
+            cP = P(a_lo - R)
+        while cur < n and int(offs[cur]) + int(lens[cur]) - R < ST_ROUND:
+            pb = P(int(offs[cur]) + int(lens[cur]) - R)
+            out[cur] = pb ^ T.shift_len(cP ^ 0xFFFFFFFF, int(lens[cur])) ^ 0xFFFFFFFF
+            cP = pb
+            cur += 1
+        G = I[63]
+        R += ST_ROUND
+        rounds += 1
+    return out, rounds

@@ -145,8 +145,16 @@ def test_general_strides_and_alignment(W, L, stride, lead):
     assert np.array_equal(to_u32(out, n), want)
 
 
+# Mixed-length tests run through both mixed-length entry points: wtp_crc32_batch_var
+# (k_pieces, any offsets) and wtp_crc32_batch_packed (k_stream; payloads that break the
+# packing take its lane-per-payload path, so every case must still be exact).
+@pytest.fixture(params=["var", "packed"])
+def VAR(W, request):
+    return W.crc32_batch_var if request.param == "var" else W.crc32_batch_packed
+
+
 @pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0)])
-def test_zipf_mixed_lengths(W, n, s):
+def test_zipf_mixed_lengths(W, VAR, n, s):
     """C5 itself at full size (1 M packets, Zipf 1.1 and 1.0), every packet vs the oracle."""
     lens = O.zipf_lengths(n, s=s)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
@@ -154,12 +162,12 @@ def test_zipf_mixed_lengths(W, n, s):
     host = O.synth_fill_np(total)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
 
 
-def _var_check(W, lens, seed=0):
+def _var_check(VAR, lens, seed=0):
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     n = int(lens.size)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
@@ -167,43 +175,43 @@ def _var_check(W, lens, seed=0):
     host = O.synth_fill_np(total, start_byte=seed)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
 
 
-def test_var_wave_split_long_subranges(W):
+def test_var_wave_split_long_subranges(W, VAR):
     """> 8 packets per thread in a workgroup's wave split (3 M packets: ~11.5 per thread),
     so the split's non-register fallback loops run; empty packets included."""
     rng = np.random.default_rng(11)
-    _var_check(W, rng.integers(0, 4, 3 << 20), seed=3)
+    _var_check(VAR, rng.integers(0, 4, 3 << 20), seed=3)
 
 
 @pytest.mark.parametrize("n", [1, 2, 17, 1000, 1025, 70_000])
-def test_var_wave_split_skewed(W, n):
+def test_var_wave_split_skewed(W, VAR, n):
     """Piece-balanced wave split with a few 4096-B packets (64 pieces) among 1-B ones:
     several waves' targets land in one packet (empty waves), and workgroups with fewer
     packets than threads."""
     lens = np.ones(n, dtype=np.uint32)
     lens[:: max(1, n // 7)] = 4096
     lens[-1] = 4096
-    _var_check(W, lens, seed=n)
+    _var_check(VAR, lens, seed=n)
 
 
-def test_mixed_golden_digest(W, golden):
+def test_mixed_golden_digest(W, VAR, golden):
     lens = np.array([1 + (i * 7919) % 1456 for i in range(2048)], dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.sum())
     d = torch.empty(total, dtype=torch.uint8, device="cuda")
     W.synth_fill(d)
     out = u32_out(2048)
-    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), 2048, out)
     got = to_u32(out, 2048)
     assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == golden["mixed_2048"]["sha256_le_u32"]
 
 
-def test_var_shuffled_offsets_and_empty(W):
+def test_var_shuffled_offsets_and_empty(W, VAR):
     rng = np.random.default_rng(5)
     n = 5000
     lens = rng.integers(0, 1485, n).astype(np.uint32)
@@ -213,7 +221,7 @@ def test_var_shuffled_offsets_and_empty(W):
     host = O.synth_fill_np(total, start_byte=99)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host, offs, lens))
 
@@ -222,7 +230,7 @@ def test_var_shuffled_offsets_and_empty(W):
 # 4096-B limit, unordered/overlapping offsets, empty payloads, an unaligned base.
 @pytest.mark.parametrize("case", ["uniform_shuffled", "all_long_packed", "all_short", "boundary_lengths", "zipf1.0_lead",
                                   "multi_segment"])
-def test_var_mixed_cases(W, case):
+def test_var_mixed_cases(W, VAR, case):
     rng = np.random.default_rng(11)
     n = {"uniform_shuffled": 100_000, "multi_segment": 1_300_000}.get(case, 70_000)
     lead = 0
@@ -249,7 +257,7 @@ def test_var_mixed_cases(W, case):
     host = O.synth_fill_np(lead + total, start_byte=n + lead)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens)), case
 
@@ -258,7 +266,7 @@ def test_var_mixed_cases(W, case):
 # caller's base, which must read as zeros); every base alignment, short and long
 # lengths, one packet per lane position.
 @pytest.mark.parametrize("lead", [0, 1, 7, 15])
-def test_var_packets_at_view_start(W, lead):
+def test_var_packets_at_view_start(W, VAR, lead):
     lens_set = [1, 5, 15, 16, 17, 100, 127, 128, 129, 255, 256, 257, 300, 1456, 4095, 4096]
     offs, lens = [], []
     for L in lens_set:
@@ -272,12 +280,12 @@ def test_var_packets_at_view_start(W, lead):
     host = O.synth_fill_np(lead + total, start_byte=lead * 3 + 1)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens))
 
 
-def test_var_bad_length_large_batch_sets_status(W):
+def test_var_bad_length_large_batch_sets_status(W, VAR):
     W.device_status(0, clear=True)
     n = 70_000
     lens = np.full(n, 700, np.uint32)
@@ -287,7 +295,7 @@ def test_var_bad_length_large_batch_sets_status(W):
     host = O.synth_fill_np(total, start_byte=1)
     d = dev_u8(host)
     out = u32_out(n)
-    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
                       torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     got = to_u32(out, n)
     want = O.batch_var(host, offs, np.where(lens > 4096, 0, lens).astype(np.uint32))
@@ -296,17 +304,108 @@ def test_var_bad_length_large_batch_sets_status(W):
     assert W.device_status(0, clear=True) & 1
 
 
-def test_var_bad_length_sets_status(W):
+def test_var_bad_length_sets_status(W, VAR):
     W.device_status(0, clear=True)
     host = O.synth_fill_np(10000)
     d = dev_u8(host)
     offs = torch.tensor([0, 10], dtype=torch.int64, device="cuda")
     lens = torch.tensor([5000, 20], dtype=torch.int32, device="cuda")
     out = u32_out(2)
-    W.crc32_batch_var(d, 10000, offs, lens, 2, out)
+    VAR(d, 10000, offs, lens, 2, out)
     got = to_u32(out, 2)
     assert got[0] == 0 and got[1] == O.crc32(host[10:30])
     assert W.device_status(0, clear=True) & 1
+
+
+def _packed(lens, first=0):
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + np.uint64(first)).astype(np.uint64)
+    return offs, lens
+
+
+def _run_packed(W, host, lead, offs, lens, total):
+    n = int(lens.size)
+    d = dev_u8(host)
+    out = u32_out(n)
+    W.crc32_batch_packed(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                         torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    return to_u32(out, n)
+
+
+@pytest.mark.parametrize("case", ["gaps", "overlaps", "swapped", "long_4096", "tiny_runs", "max_fast_4095"])
+def test_packed_breaks_and_edges(W, case):
+    """wtp_crc32_batch_packed on batches that break the packing at a few places (a gap,
+    an overlap, two swapped payloads, 4096-B payloads beyond the fast path's 4095):
+    the waves hand the rest of their range to the lane-per-payload path; runs of
+    0-3-B payloads (many group rotations per 8 KiB round) and 4095-B payloads (the
+    largest the length shift covers)."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    n = 300_000
+    lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
+    if case == "tiny_runs":
+        lens = rng.integers(0, 4, n).astype(np.uint32)
+        lens[rng.integers(0, n, 50)] = 1456
+    if case == "max_fast_4095":
+        lens = np.where(rng.random(n) < 0.3, 4095, lens).astype(np.uint32)
+    offs, lens = _packed(lens, first=5)
+    bad = np.sort(rng.choice(n - 2, 40, replace=False)) + 1
+    if case == "gaps":
+        offs[bad[0]:] += np.uint64(3)
+        for b in bad[1:]:
+            offs[b:] += np.uint64(int(rng.integers(1, 200)))
+    elif case == "overlaps":
+        for b in bad:
+            offs[b] -= np.uint64(min(int(lens[b - 1]), 7))
+    elif case == "swapped":
+        for b in bad:
+            offs[[b, b + 1]] = offs[[b + 1, b]]
+            lens[[b, b + 1]] = lens[[b + 1, b]]
+    elif case == "long_4096":
+        lens[bad] = 4096
+        offs, lens = _packed(lens, first=5)
+    lead = 11
+    total = int((offs + lens).max()) + 16
+    host = O.synth_fill_np(lead + total, start_byte=n)
+    got = _run_packed(W, host, lead, offs, lens, total)
+    assert np.array_equal(got, O.batch_var(host[lead:], offs, lens)), case
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 127, 129, 511, 513, 4097])
+def test_packed_small_batches(W, n):
+    """Small packed batches (fewer payloads than lanes, waves or workgroups), every base
+    alignment and a first offset that is not 0."""
+    rng = np.random.default_rng(n)
+    for lead in (0, 5, 15):
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        offs, lens = _packed(lens, first=int(rng.integers(0, 300)))
+        total = int(offs[-1] + lens[-1]) + int(rng.integers(0, 40))
+        host = O.synth_fill_np(lead + total, start_byte=n + lead)
+        got = _run_packed(W, host, lead, offs, lens, total)
+        assert np.array_equal(got, O.batch_var(host[lead:], offs, lens)), (n, lead)
+
+
+def test_packed_view_over_4gib(W):
+    """A packed batch whose buffer is > 4 GiB (payloads at offsets past 2^32; the general
+    kernel's views stop at 2 GiB): 3.2 M x 1456-B payloads generated on the device,
+    every CRC equal to the braided fixed-length kernel's, and sampled payloads vs the
+    oracle (regenerated from the generator at their global offsets)."""
+    n, L = 3_200_000, 1456
+    total = n * L
+    assert total > (1 << 32)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    lens = np.full(n, L, np.uint32)
+    offs, lens = _packed(lens)
+    out = u32_out(n)
+    W.crc32_batch_packed(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                         torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    ref = u32_out(n)
+    W.crc32_batch_fixed(d, L, L, n, ref)
+    got = to_u32(out, n)
+    assert np.array_equal(got, to_u32(ref, n))
+    for i in (0, 1, 2949840, 2949841, n - 1):  # payload 2949840 straddles 2^32, 2949841 starts past it
+        assert int(got[i]) == O.crc32(O.synth_fill_np(L, start_byte=i * L)), i
+    del d
 
 
 # ---- receiver verify, packet builder, host pipelines -----------------------------------

@@ -60,3 +60,28 @@ def test_pieces_rounds_model(T, case):
     assert got == want
     if case in ("packed_zipf", "strided_odd"):
         assert hits == rounds - 1  # every round after the first is prefetched
+
+
+@pytest.mark.parametrize("case", ["zipf", "tiny", "long_4095", "one", "empty_mix"])
+def test_stream_model(case):
+    """k_stream's algebra (prefix values, block anchors, feed, nibble length shift) on
+    packed batches at several view alignments, vs the oracle."""
+    import kernel_model as K
+    T = K.StreamTables()
+    rng = np.random.default_rng(len(case))
+    n = {"one": 1, "long_4095": 12}.get(case, 150)
+    if case == "zipf":
+        lens = O.zipf_lengths(n, s=1.1)
+    elif case == "tiny":
+        lens = rng.integers(0, 4, n)
+    elif case == "long_4095":
+        lens = np.full(n, 4095)
+    elif case == "one":
+        lens = np.array([33])
+    else:
+        lens = np.where(rng.random(n) < 0.5, 0, rng.integers(1, 300, n))
+    for first, view_addr in ((0, 0), (77, 16), (130, 48)):
+        offs = first + np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+        buf = O.synth_fill_np(int(offs[-1] + lens[-1]) + 9, start_byte=first).tobytes()
+        out, _ = K.stream_wave(T, buf, offs, lens, view_addr=view_addr)
+        assert out == [O.crc32(buf[o:o + L]) for o, L in zip(offs, lens)], (case, first)
