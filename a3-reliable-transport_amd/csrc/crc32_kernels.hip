@@ -1685,6 +1685,11 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     const uint8_t *b = static_cast<const uint8_t *>(d_base);
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // The general kernel addresses a view of < 2 GiB (32-bit buffer offsets).  Larger
+    // buffers go to the stream kernel, which takes 64-bit offsets: packed runs on its
+    // fast path, any other layout on its lane-per-payload path, exact either way.
+    if (((lead + base_bytes + 15) & ~uint64_t(15)) >= (1ull << 31))
+        return launch_stream(*s, b, base_bytes, d_offsets, d_lengths, n, d_out, st);
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
         rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,

@@ -89,20 +89,24 @@ uint32_t wtp_crc32(const void *buf, size_t size);
 int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, size_t n,
                           uint32_t *d_out, void *stream);
 
-/* Mixed lengths: payload i = d_base[d_offsets[i] .. d_offsets[i] + d_lengths[i]).
-   `base_bytes` = size of the d_base buffer (bounds for the loads; < 2 GiB, so only
-   the low 32 bits of each offset are read).  d_lengths[i] <= WTP_MAX_KERNEL_LEN. */
+/* Mixed lengths: payload i = d_base[d_offsets[i] .. d_offsets[i] + d_lengths[i]), any
+   order, overlaps allowed.  `base_bytes` = size of the d_base buffer (bounds for the
+   loads).  Buffers below 2 GiB run the general (piece-stream) kernel; larger ones run
+   the stream kernel of wtp_crc32_batch_packed (64-bit offsets), so there is no size
+   limit.  d_lengths[i] <= WTP_MAX_KERNEL_LEN. */
 int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                         const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
-/* Mixed lengths stored back to back (a receive buffer, a record file): as
-   wtp_crc32_batch_var with d_offsets[i+1] == d_offsets[i] + d_lengths[i] (offsets =
+/* The stream kernel explicitly, for mixed lengths stored back to back (a receive
+   buffer, a record file): d_offsets[i+1] == d_offsets[i] + d_lengths[i] (offsets =
    exclusive prefix sum of the lengths, any first offset).  Each wave hashes its region
    of the byte stream once and reads every payload's CRC off prefix values (no per-
    payload windows, masks or padding).  No limit on base_bytes (64-bit offsets) or n.
    Payloads that break the packing, or are longer than 4095 B, are still computed
    exactly on a slower lane-per-payload path, so results are correct for any offsets;
-   lengths > WTP_MAX_KERNEL_LEN give crc 0 and set the status flag. */
+   lengths > WTP_MAX_KERNEL_LEN give crc 0 and set the status flag.
+   wtp_crc32_batch_var uses this kernel by itself for buffers >= 2 GiB; below that the
+   general kernel is currently the faster one on packed batches too (C5: DESIGN.md). */
 int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 

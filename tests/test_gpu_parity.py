@@ -384,11 +384,12 @@ def test_packed_small_batches(W, n):
         assert np.array_equal(got, O.batch_var(host[lead:], offs, lens)), (n, lead)
 
 
-def test_packed_view_over_4gib(W):
+def test_packed_view_over_4gib(W, VAR):
     """A packed batch whose buffer is > 4 GiB (payloads at offsets past 2^32; the general
-    kernel's views stop at 2 GiB): 3.2 M x 1456-B payloads generated on the device,
-    every CRC equal to the braided fixed-length kernel's, and sampled payloads vs the
-    oracle (regenerated from the generator at their global offsets)."""
+    kernel's views stop at 2 GiB, so wtp_crc32_batch_var hands it to the stream kernel):
+    3.2 M x 1456-B payloads generated on the device, every CRC equal to the braided
+    fixed-length kernel's, and sampled payloads vs the oracle (regenerated from the
+    generator at their global offsets)."""
     n, L = 3_200_000, 1456
     total = n * L
     assert total > (1 << 32)
@@ -397,8 +398,7 @@ def test_packed_view_over_4gib(W):
     lens = np.full(n, L, np.uint32)
     offs, lens = _packed(lens)
     out = u32_out(n)
-    W.crc32_batch_packed(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
-                         torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    VAR(d, total, torch.from_numpy(offs.view(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
     ref = u32_out(n)
     W.crc32_batch_fixed(d, L, L, n, ref)
     got = to_u32(out, n)
@@ -406,6 +406,33 @@ def test_packed_view_over_4gib(W):
     for i in (0, 1, 2949840, 2949841, n - 1):  # payload 2949840 straddles 2^32, 2949841 starts past it
         assert int(got[i]) == O.crc32(O.synth_fill_np(L, start_byte=i * L)), i
     del d
+
+
+def test_var_unordered_view_over_2gib(W):
+    """wtp_crc32_batch_var on a 2.3 GB buffer (no longer EINVAL): 100 K payloads at
+    unordered, overlapping offsets across the whole buffer, lengths 0..1500 and a few
+    over-long ones -> the stream kernel's lane-per-payload path, every CRC vs the oracle."""
+    W.device_status(0, clear=True)
+    total = 2_300_000_000
+    rng = np.random.default_rng(23)
+    n = 100_000
+    lens = rng.integers(0, 1501, n).astype(np.uint32)
+    lens[::9973] = 5000
+    offs = rng.integers(0, total - 6000, n).astype(np.uint64)
+    offs[:50] = np.arange(50, dtype=np.uint64) * np.uint64(3)  # some near the start, overlapping
+    offs[50:100] = np.uint64(total - 1600) + np.arange(50, dtype=np.uint64)  # some ending near the end
+    lens[50:100] = np.minimum(lens[50:100], 1500)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    out = u32_out(n)
+    W.crc32_batch_var(d, total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    got = to_u32(out, n)
+    host = d.cpu().numpy()
+    del d
+    want = O.batch_var(host, offs, np.where(lens > 4096, 0, lens).astype(np.uint32))
+    assert np.array_equal(got, want)
+    assert W.device_status(0, clear=True) & 1
 
 
 # ---- receiver verify, packet builder, host pipelines -----------------------------------

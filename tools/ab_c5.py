@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--s", type=float, default=1.1)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--n", type=int, default=1 << 20)
+ap.add_argument("--entry", default="var", choices=["var", "packed"])
 a = ap.parse_args()
 libs = sorted(glob.glob(os.path.join(ROOT, "a3-reliable-transport_amd", "lib", "ab", "*.so")))
 L = {os.path.basename(p)[:-3]: C.CDLL(p) for p in libs}
@@ -39,7 +40,8 @@ torch.cuda.synchronize()
 
 
 def call(k):
-    return L[k].wtp_crc32_batch_var(C.c_void_p(d.data_ptr()), C.c_size_t(total), C.c_void_p(do.data_ptr()),
+    f = L[k].wtp_crc32_batch_packed if a.entry == "packed" else L[k].wtp_crc32_batch_var
+    return f(C.c_void_p(d.data_ptr()), C.c_size_t(total), C.c_void_p(do.data_ptr()),
                                     C.c_void_p(dl.data_ptr()), C.c_size_t(a.n), C.c_void_p(outs[k].data_ptr()), None)
 
 
