@@ -155,15 +155,53 @@ __device__ __forceinline__ uint32_t stag_apply(const char *lds, const uint32_t (
 }
 
 // Fill one table set (1024 words from global: table t at g[256 t]) into the staggered image.
+// Store j (of 2048) writes the 16-B half h = j & 1 of table t = (j >> 1) & 3's 8 copies of
+// entry e = j >> 3, so each 8-lane ds_write_b128 group covers 128 contiguous bytes (one
+// entry per 32 B, lanes 256 B apart, was 8-way bank-conflicted: 3.4 us per launch).
+__device__ __forceinline__ uint32_t stag_fill_word(uint32_t j) { return ((j >> 1) & 3u) * 256u + (j >> 3); }
+__device__ __forceinline__ uint32_t stag_fill_off(uint32_t j) { return (j >> 3) * 256u + ((j >> 1) & 3u) * 32u + (j & 1u) * 16u; }
 __device__ __forceinline__ void fill_stag(char *lds, uint32_t region, uint32_t set, const uint32_t *__restrict__ g) {
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
-        const uint32_t t = i >> 8, e = i & 255u;
-        const uint32_t v = g[i];
-        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + region * 65536u + e * 256u + set * 128u + t * 32u);
-        const u32x4 q = {v, v, v, v};
-        dst[0] = q;
-        dst[1] = q;
+    for (uint32_t j = threadIdx.x; j < 2048; j += blockDim.x) {
+        const uint32_t v = g[stag_fill_word(j)];
+        *reinterpret_cast<u32x4 *>(lds + region * 65536u + set * 128u + stag_fill_off(j)) = u32x4{v, v, v, v};
     }
+}
+
+// Staggered fill of NS table sets with every global load of a thread issued before any
+// LDS write.  The tables are usually evicted from L2 by the stream between launches, and
+// the load-write loop of fill_stag paid one memory latency per word: entry to first
+// round took 5.9 us in every braided launch (tools/bprobe.py), a third of a C2 launch.
+struct StagSet {
+    const uint32_t *g;  // 4 byte tables (1024 words)
+    uint32_t off;       // region * 65536 + set * 128
+};
+// load() issues the loads, store() writes LDS: a kernel issues the table loads before
+// its first data loads, since vmcnt completes in order and the table writes would
+// otherwise wait for the first round's data (the fill ended 4.4 us after entry).
+template <int NS, int THREADS>
+struct StagFill {
+    static_assert(THREADS <= 1024 && 2048 % THREADS == 0, "StagFill");
+    static constexpr int PER = NS * 2048 / THREADS;  // 16-B stores per thread (see fill_stag)
+    uint32_t v[PER];
+    __device__ __forceinline__ void load(const StagSet (&sets)[NS]) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            v[k] = sets[(k * THREADS) >> 11].g[stag_fill_word((uint32_t(k * THREADS) + threadIdx.x) & 2047u)];
+    }
+    __device__ __forceinline__ void store(char *lds, const StagSet (&sets)[NS]) const {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const uint32_t j = (uint32_t(k * THREADS) + threadIdx.x) & 2047u;
+            *reinterpret_cast<u32x4 *>(lds + sets[(k * THREADS) >> 11].off + stag_fill_off(j)) =
+                u32x4{v[k], v[k], v[k], v[k]};
+        }
+    }
+};
+template <int NS, int THREADS>
+__device__ __forceinline__ void fill_stag_batch(char *lds, const StagSet (&sets)[NS]) {
+    StagFill<NS, THREADS> f;
+    f.load(sets);
+    f.store(lds, sets);
 }
 
 // ------------------------------------------------------------------------------------
@@ -356,6 +394,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
     const uint32_t nwave = blockDim.x >> 6;
     const uint32_t j = lane & (kG - 1);  // braid group (column) within the packet
     const uint32_t q = lane >> 4;        // packet slot within the wave (0..3)
@@ -481,12 +520,31 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
     uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
+    // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
+    // first, the first round's data loads overlap the LDS writes
+    const StagSet sets[4] = {{gtab + OFF_BRAID, 0u},
+                             {gtab + OFF_INV + 0 * 1024, 128u},
+                             {gtab + OFF_INV + 2 * 1024, 65536u},
+                             {gtab + OFF_INV + 5 * 1024, 65536u + 128u}};
+    constexpr int kT = BEpi::kCopy ? 128 : 512;  // the launcher's workgroup sizes
+    StagFill<4, kT> fill;
+    const bool batched = blockDim.x == kT;  // other sizes: tools/kbench.hip A/B builds
+#ifndef WTP_BR_PROLOGUE_DIAG  // probe builds only: 1 = no table loads, 2 = no table fill at all
+#define WTP_BR_PROLOGUE_DIAG 0
+#endif
+    if (batched && WTP_BR_PROLOGUE_DIAG == 0) fill.load(sets);
+    if (WTP_BR_PROLOGUE_DIAG == 1)
+        for (int kk = 0; kk < fill.PER; ++kk) fill.v[kk] = threadIdx.x + kk;
     epi.pre(group_packet(r), pre);
     load_round(r, A);
-    fill_stag(lds, 0, 0, gtab + OFF_BRAID);
-    fill_stag(lds, 0, 1, gtab + OFF_INV + 0 * 1024);  // x^-32
-    fill_stag(lds, 1, 0, gtab + OFF_INV + 2 * 1024);  // x^-128
-    fill_stag(lds, 1, 1, gtab + OFF_INV + 5 * 1024);  // x^-1024
+    PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
+    if (WTP_BR_PROLOGUE_DIAG == 2) {
+    } else if (batched) {
+        fill.store(lds, sets);
+    } else {
+        for (int q2 = 0; q2 < 4; ++q2) fill_stag(lds, sets[q2].off >> 16, (sets[q2].off >> 7) & 1u, sets[q2].g);
+    }
+    PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
     __syncthreads();
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
 
@@ -502,6 +560,7 @@ __global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict_
         if (!(DIAG & 4)) rotate_prio(++prio_round);
         load_round(r + rstep, B);
         crc_round(r, A);
+        if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
         r += rstep;
         if (r >= rounds) break;
         load_round(r + rstep, A);
@@ -728,15 +787,32 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
     PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
     WaveSplit split;
-    if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
-    PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
-    fill_stag(lds, 0, 0, gtab + OFF_S4);
-    fill_stag(lds, 0, 1, gtab + OFF_FWD);
     {
-        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kPcOps);
+        // every table load first (one memory latency, and ahead of the length loads of the
+        // wave split, since vmcnt completes in order; see StagFill): the staggered sets,
+        // the plain scan operators and the head-init table
+        constexpr uint32_t kOpQ = 5 * 256, kOpPer = (kOpQ + kPcThreads - 1) / kPcThreads;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024);
-        for (uint32_t i = threadIdx.x; i < 5 * 256; i += blockDim.x) dst[i] = src[i];
-        if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = gtab[OFF_HINIT + threadIdx.x];
+        const StagSet sets[2] = {{gtab + OFF_S4, 0u}, {gtab + OFF_FWD, 128u}};
+        StagFill<2, kPcThreads> fill;
+        fill.load(sets);
+        u32x4 q[kOpPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kOpPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kPcThreads;
+            q[k] = src[i < kOpQ ? i : 0];
+        }
+        const uint32_t hv = gtab[OFF_HINIT + (threadIdx.x <= kPieceS ? threadIdx.x : 0)];
+        if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
+        PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
+        fill.store(lds, sets);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kPcOps);
+#pragma unroll
+        for (uint32_t k = 0; k < kOpPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kPcThreads;
+            if (i < kOpQ) dst[i] = q[k];
+        }
+        if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = hv;
     }
     uint64_t lo, hi;
     if constexpr (Prov::kVarLen) {
@@ -1004,14 +1080,31 @@ __global__ __launch_bounds__(kStThreads) void k_stream(const uint8_t *__restrict
     uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kStBal);
     const uint64_t span = g1 - g0;
     const uint64_t smp = g0 + ((span * threadIdx.x) >> 9);
-    const uint64_t o0 = off_of(g0), oe = off_of(g1 - 1) + len_of(g1 - 1), os = off_of(smp);
     if (threadIdx.x <= kStWaves) starts[threadIdx.x] = threadIdx.x == 0 ? g0 : g1;
-    fill_stag(lds, 0, 0, gtab + OFF_S4);
-    fill_stag(lds, 0, 1, gtab + OFF_T256);
+    uint64_t o0, oe, os;
     {
-        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kStNib);
+        // table loads ahead of the sample loads (vmcnt completes in order; see StagFill)
+        constexpr uint32_t kNQ = kStNibOps * 32, kNPer = (kNQ + kStThreads - 1) / kStThreads;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_NIB);
-        for (uint32_t i = threadIdx.x; i < kStNibOps * 32; i += blockDim.x) dst[i] = src[i];
+        const StagSet sets[2] = {{gtab + OFF_S4, 0u}, {gtab + OFF_T256, 128u}};
+        StagFill<2, kStThreads> fill;
+        fill.load(sets);
+        u32x4 q[kNPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kNPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kStThreads;
+            q[k] = src[i < kNQ ? i : 0];
+        }
+        o0 = off_of(g0);
+        oe = off_of(g1 - 1) + len_of(g1 - 1);
+        os = off_of(smp);
+        fill.store(lds, sets);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kStNib);
+#pragma unroll
+        for (uint32_t k = 0; k < kNPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kStThreads;
+            if (i < kNQ) dst[i] = q[k];
+        }
     }
     __syncthreads();
     {
