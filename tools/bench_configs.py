@@ -48,15 +48,27 @@ def timed(fn, reps, warm=3):
     return ts[len(ts) // 2], tot / reps
 
 
-def graph_time(fn, G=50, reps=20):
+def graph_time(fn, G=50, reps=7, per=10):
     """Per-launch ms of fn replayed from a captured HIP graph of G launches (no host work
-    between kernels)."""
+    between kernels): median over `reps` timings of `per` consecutive replays (timing each
+    replay on its own adds the graph-launch gap, ~1.7 us per launch at G = 50)."""
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         for _ in range(G):
             fn()
-    _, gmean = timed(graph.replay, reps)
-    return gmean / G, graph
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(per):
+            graph.replay()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / (per * G))
+    return float(np.median(ts)), graph
 
 
 def c2():
