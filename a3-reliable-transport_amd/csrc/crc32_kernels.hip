@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -287,7 +288,7 @@ struct VerifyBEpi {
     uint64_t stride;
     uint8_t *ok;
     uint32_t *crc;  // may be null
-    uint32_t *fix;  // fix[0] = count, fix[1..] = datagram indices
+    uint32_t *fix;  // fix[0] = count, fix[1] = the fix-up pass's done counter, fix[2..] = indices
     uint32_t cinit;
     uint64_t n;
     uint32_t full;  // recv_len of the datagrams this pass decides (16 + len)
@@ -307,7 +308,7 @@ struct VerifyBEpi {
             ok[p] = bswap32(q.h) == c ? 1 : 0;
             if (crc) crc[p] = c;
         } else {
-            fix[1 + atomicAdd(fix, 1u)] = uint32_t(p);
+            fix[2 + atomicAdd(fix, 1u)] = uint32_t(p);
         }
     }
 };
@@ -781,7 +782,13 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     const uint32_t nw = blockDim.x >> 6;
     const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
     const uint64_t g0 = n * w0 / tw, g1 = n * (w0 + nw) / tw;  // this workgroup's packets
-    if (g0 == g1) return;                                       // no packets for this block
+    if (g0 == g1) {  // no packets for this block
+        if constexpr (Prov::kCounted) {
+            __syncthreads();  // every thread has read the count
+            if (threadIdx.x == 0) prov.done(gridDim.x);
+        }
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
@@ -822,6 +829,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
         hi = n * (w0 + wave + 1) / tw;
         __syncthreads();
     }
+    if constexpr (Prov::kCounted)
+        if (threadIdx.x == 0) prov.done(gridDim.x);  // after the barrier: the block has read the count
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
 
     const StagKeys K(lane);
@@ -1425,6 +1434,14 @@ struct DevState {
     uint32_t *status = nullptr;
     int cus = 0;
     hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed
+    // verify fix-up lists, one per stream (kernels of one stream never overlap): zeroed
+    // once when allocated, then reset by the fix-up pass itself (IdxDgramProvL)
+    struct FixSlot {
+        uint32_t *buf = nullptr;
+        uint64_t cap = 0;  // u32 entries
+    };
+    std::mutex fix_mu;
+    std::unordered_map<hipStream_t, FixSlot> fix_slots;
 };
 constexpr int kMaxDev = 64;
 DevState g_dev[kMaxDev];
@@ -1595,6 +1612,7 @@ namespace dev {
 // raw words into (offset in the view, length, valid, aux, output slot) when the round
 // uses them.  count(n) is the number of packets (device-side for the fix-up pass).
 struct FixedProvL {
+    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
@@ -1609,6 +1627,7 @@ struct FixedProvL {
     }
 };
 struct ArrayProvL {
+    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     const uint64_t *__restrict__ offs;
@@ -1634,6 +1653,7 @@ struct ArrayProvL {
 // the last datagram, reads there return 0 and are never selected) and are
 // funnel-shifted at decode.
 struct DgramProvL {
+    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
@@ -1661,18 +1681,29 @@ struct DgramProvL {
 // The fix-up pass of the braided verify: datagrams fix[1 .. fix[0]] of the ring (in
 // whatever order the atomics left them).  The index load makes this provider's other
 // loads dependent (it only sees the rare short or malformed datagrams).
+// The list lives in a per-(device, stream) slot that outlives the call: fix[0] = count,
+// fix[1] = workgroups done, fix[2 ..] = indices.  Every workgroup of this pass reads the
+// count, then adds itself to fix[1]; the last one zeroes both, so the slot is ready for
+// the next call on the stream with no memset or allocation per call.
 struct IdxDgramProvL {
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = true;
+    static constexpr bool kCounted = true;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
-    const uint32_t *__restrict__ fix;
+    uint32_t *fix;
     __device__ __forceinline__ uint64_t count(uint64_t n) const {
         const uint64_t c = *(const __attribute__((address_space(1))) uint32_t *)fix;  // written by the braid pass
         return c < n ? c : n;
     }
+    __device__ __forceinline__ void done(uint32_t grid) const {
+        if (atomicAdd(fix + 1, 1u) == grid - 1) {
+            __atomic_store_n(fix, 0u, __ATOMIC_RELAXED);
+            __atomic_store_n(fix + 1, 0u, __ATOMIC_RELAXED);
+        }
+    }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
-        const uint32_t idx = fix[1 + p];
+        const uint32_t idx = fix[2 + p];
         const uint32_t h = uint32_t(lead + uint64_t(idx) * stride + 12) & ~3u;
         r.a = idx;
         r.b = rl[idx];
@@ -1821,27 +1852,58 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     if (stride % 16 == 0 && stride >= 32 && stride <= 16384 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
         const uint32_t flen = uint32_t(std::min<size_t>(stride - 16, WTP_MAX_PAYLOAD));
         const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
+        const uint64_t need = 2 + std::min<uint64_t>(per, n);
+        // The fix-up list: the stream's persistent slot (zeroed once, reset by the fix-up
+        // pass), or, while the stream is being captured into a graph (whose replays need
+        // not follow this stream's order), scratch of this call zeroed by a memset node.
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        WTP_HIP(hipStreamIsCapturing(st, &cs));
+        const bool scratch = cs != hipStreamCaptureStatusNone;
+        std::unique_lock<std::mutex> lk(s->fix_mu, std::defer_lock);  // held until the launches are queued
         uint32_t *fix = nullptr;
-        WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&fix), 4 * (std::min<uint64_t>(per, n) + 1), s->pool, st));
+        if (scratch) {
+            WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&fix), 4 * need, s->pool, st));
+            if (hipMemsetAsync(fix, 0, 8, st) != hipSuccess) {
+                (void)hipFreeAsync(fix, st);
+                return fail(WTP_EHIP, "hipMemsetAsync failed");
+            }
+        } else {
+            lk.lock();
+            DevState::FixSlot &slot = s->fix_slots[st];
+            if (slot.cap < need) {
+                if (slot.buf) WTP_HIP(hipFreeAsync(slot.buf, st));  // after the stream's earlier uses
+                slot.buf = nullptr;
+                slot.cap = 0;
+                uint32_t *nb = nullptr;
+                WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&nb), 4 * need, s->pool, st));
+                if (hipMemsetAsync(nb, 0, 8, st) != hipSuccess) {
+                    (void)hipFreeAsync(nb, st);
+                    return fail(WTP_EHIP, "hipMemsetAsync failed");
+                }
+                slot.buf = nb;
+                slot.cap = need;
+            }
+            fix = slot.buf;
+        }
         for (uint64_t p = 0; p < n && !rc; p += per) {
             const uint64_t cnt = std::min<uint64_t>(per, n - p);
             const uint8_t *sb = b + p * stride;
             uint8_t *ok = d_ok + p;
             uint32_t *crc = d_crc_out ? d_crc_out + p : nullptr;
-            if (hipMemsetAsync(fix, 0, 4, st) != hipSuccess) {
-                rc = fail(WTP_EHIP, "hipMemsetAsync failed");
-                break;
-            }
             rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
                                     dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt, 16u + flen}, st);
             if (!rc)
                 rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix}, cnt,
                                    dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);
         }
-        const hipError_t fe = hipFreeAsync(fix, st);
-        if (rc) return rc;
-        if (fe != hipSuccess) return fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
-        return WTP_OK;
+        if (scratch) {
+            const hipError_t fe = hipFreeAsync(fix, st);
+            if (rc) return rc;
+            if (fe != hipSuccess) return fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
+        } else if (rc) {
+            (void)hipMemsetAsync(fix, 0, 8, st);  // a braid pass whose fix-up pass never ran left a count
+        }
+        return rc;
     }
     const uint64_t per = std::min<uint64_t>(kSubBatch, std::max<uint64_t>(1, (1ull << 30) / stride));
     for (uint64_t p = 0; p < n; p += per) {

@@ -572,6 +572,75 @@ def test_verify_wreceiver_1504_slots(W, n):
     assert np.array_equal(ok2, want_ok) and np.array_equal(crc2, want_crc)
 
 
+def test_verify_fixup_slot_reuse(W):
+    """The fix-up list is a per-stream slot the fix-up pass resets itself: back-to-back
+    calls on one stream (growing and shrinking batches), calls on a second stream, an
+    all-full ring (empty list) between them, and a CUDA-graph capture (per-call scratch)
+    replayed twice all stay bit-exact."""
+    rng = np.random.default_rng(2024)
+    stride = 1504
+    rings = {}
+    for n in (64, 3001, 97, 20000, 1):
+        buf, rl = _wtp_ring(n, stride, rng)
+        want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+        rings[n] = (dev_u8(buf), torch.from_numpy(rl.view(np.int32)).cuda(), want_ok, want_crc)
+    full_n = 500
+    full = torch.empty(full_n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(full)
+    fwire = torch.zeros(full_n * stride, dtype=torch.uint8, device="cuda")
+    fwl = torch.empty(full_n, dtype=torch.int32, device="cuda")
+    W.build_data_packets(full, full_n * 1456, 0, fwire, stride, fwl)
+
+    def run(n, stream=None):
+        d, r, _, _ = rings[n]
+        ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        crc = u32_out(n)
+        W.verify_batch(d, stride, r, n, ok, crc, stream=stream)
+        return ok, crc
+
+    def check(n, ok, crc):
+        _, _, want_ok, want_crc = rings[n]
+        assert np.array_equal(ok.cpu().numpy(), want_ok), n
+        assert np.array_equal(to_u32(crc, n), want_crc), n
+
+    outs = []
+    for rep in range(3):
+        for n in (64, 3001, 97, 20000, 1):
+            outs.append((n, *run(n)))
+            fok = torch.zeros(full_n, dtype=torch.uint8, device="cuda")
+            W.verify_batch(fwire, stride, fwl, full_n, fok)
+            outs.append((None, fok, None))
+    s2 = torch.cuda.Stream()
+    s2.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s2):
+        for n in (3001, 64):
+            outs.append((n, *run(n)))
+    torch.cuda.synchronize()
+    for n, ok, crc in outs:
+        if n is None:
+            assert bool(ok.all())
+        else:
+            check(n, ok, crc)
+    # graph capture: the fix-up list is scratch of the captured call, zeroed by the graph
+    d, r, _, _ = rings[3001]
+    gok = torch.full((3001,), 7, dtype=torch.uint8, device="cuda")
+    gcrc = u32_out(3001)
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        g.capture_begin()
+        W.verify_batch(d, stride, r, 3001, gok, gcrc)
+        g.capture_end()
+    torch.cuda.current_stream().wait_stream(cs)
+    for _ in range(2):
+        gok.fill_(7)
+        g.replay()
+        torch.cuda.synchronize()
+        check(3001, gok, gcrc)
+        check(97, *run(97))  # the stream's slot is untouched by the graph
+
+
 def test_verify_misaligned_ring_takes_general_path(W):
     rng = np.random.default_rng(11)
     n, stride = 700, 1472
