@@ -183,6 +183,7 @@ def verify():
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     f = lambda: W.verify_batch(wire, stride, wl, n, ok)  # noqa: E731
     med, mean = timed(f, 100)
+    gv, _ = graph_time(f)
     good = int(ok.sum().item())
     fb = lambda: W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)  # noqa: E731
     bmed, bmean = timed(fb, 50)
@@ -201,15 +202,18 @@ def verify():
     rl2 = torch.full((n,), stride, dtype=torch.int32, device="cuda")
     f2 = lambda: W.verify_batch(w2, 1504, rl2, n, ok)  # noqa: E731
     med2, mean2 = timed(f2, 100)
+    gv2, _ = graph_time(f2)
     good2 = int(ok.sum().item())
     del w2, rl2
     wl = torch.empty(n, dtype=torch.int32, device="cuda")
     return [{"config": "receiver verify, 1M x 1472-B datagrams device-resident", "packets": n,
              "ms_per_launch": round(mean, 4), "payload_GiBps": round(n * 1456 / (mean * 1e-3) / GIB, 1),
-             "read_GBps": round(n * (stride + 4) / (mean * 1e-3) / GB, 1), "all_ok": good == n},
+             "read_GBps": round(n * (stride + 4) / (mean * 1e-3) / GB, 1), "graph_ms_per_launch": round(gv, 4),
+             "graph_frac_hbm": round(n * (stride + 4) / (gv * 1e-3) / GB / PEAK, 4), "all_ok": good == n},
             {"config": "receiver verify, 1M x 1472-B datagrams in 1504-B slots (wReceiver ring)", "packets": n,
              "ms_per_launch": round(mean2, 4), "payload_GiBps": round(n * 1456 / (mean2 * 1e-3) / GIB, 1),
-             "read_GBps": round(n * (stride + 4) / (mean2 * 1e-3) / GB, 1), "all_ok": good2 == n},
+             "read_GBps": round(n * (stride + 4) / (mean2 * 1e-3) / GB, 1), "graph_ms_per_launch": round(gv2, 4),
+             "graph_frac_hbm": round(n * (stride + 4) / (gv2 * 1e-3) / GB / PEAK, 4), "all_ok": good2 == n},
             {"config": "fused DATA packet builder, 1M x 1456 B -> 1472-B wire slots", "packets": n,
              "ms_per_launch": round(bmean, 4), "GBps_read_plus_write": round(n * (1456 + 1472) / (bmean * 1e-3) / GB, 1),
              "d2d_copy_same_bytes_GBps_read_plus_write": round(2 * n * 1456 / (cmean * 1e-3) / GB, 1),
