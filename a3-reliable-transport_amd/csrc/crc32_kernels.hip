@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -1433,6 +1434,8 @@ struct DevState {
     uint32_t *tabs = nullptr;
     uint32_t *status = nullptr;
     int cus = 0;
+    std::atomic<int> reserve{0};  // CUs left free of the persistent kernels (wtp_reserve_cus)
+    unsigned grid_cus() const { return unsigned(std::max(1, cus - reserve.load(std::memory_order_relaxed))); }
     hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed
     // verify fix-up lists, one per stream (kernels of one stream never overlap): zeroed
     // once when allocated, then reset by the fix-up pass itself (IdxDgramProvL)
@@ -1556,7 +1559,7 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
     const unsigned threads = BEpi::kCopy ? kBuildThreads : kBraidThreads;
     const uint64_t rounds = (n + 3) / 4;
     const uint64_t want = (rounds + threads / 64 - 1) / (threads / 64);
-    const unsigned grid = unsigned(want < uint64_t(s.cus) ? want : uint64_t(s.cus));
+    const unsigned grid = unsigned(want < uint64_t(s.grid_cus()) ? want : uint64_t(s.grid_cus()));
     epi.cinit = init_const(len);
     switch (rows) {
         case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
@@ -1582,7 +1585,7 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
     if (span >= (1ull << 31)) return fail(WTP_EINVAL, "general kernel span %llu B >= 2 GiB (split the batch)", (unsigned long long)span);
     const uint64_t waves_want = (n + 63) / 64;
     uint64_t grid = (waves_want + dev::kPcThreads / 64 - 1) / (dev::kPcThreads / 64);
-    if (grid > uint64_t(s.cus)) grid = uint64_t(s.cus);
+    if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(dev::kPcThreads), 0, st, b16, uint32_t(span),
                        prov, n, epi, s.tabs, s.status);
@@ -1595,7 +1598,7 @@ int launch_stream(DevState &s, const uint8_t *base, uint64_t nbytes, const uint6
                   uint64_t n, uint32_t *out, hipStream_t st) {
     const uint64_t lead = reinterpret_cast<uintptr_t>(base) & 15u;
     uint64_t grid = (n + dev::kStWaves * 64 - 1) / (dev::kStWaves * 64);  // >= 64 payloads per wave
-    if (grid > uint64_t(s.cus)) grid = uint64_t(s.cus);
+    if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL((dev::k_stream<0>), dim3(unsigned(grid)), dim3(dev::kStThreads), 0, st, base - lead,
                        lead + nbytes, offs, lens, lead, n, out, s.tabs, s.status);
@@ -1748,6 +1751,15 @@ int wtp_device_count(void) {
 }
 
 int wtp_init(int device) { return init_device(device); }
+
+int wtp_reserve_cus(int device, int ncus) {
+    int rc = init_device(device);
+    if (rc) return rc;
+    DevState &s = g_dev[device];
+    if (ncus < 0 || ncus >= s.cus) return fail(WTP_EINVAL, "ncus %d outside [0, %d)", ncus, s.cus);
+    s.reserve.store(ncus, std::memory_order_relaxed);
+    return WTP_OK;
+}
 
 int wtp_device_status(int device, uint32_t *flags, int clear) {
     if (!flags) return fail(WTP_EINVAL, "flags is null");

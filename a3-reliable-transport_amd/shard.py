@@ -83,6 +83,23 @@ def gather_crcs(local, world: int, rank: int, dst: int = 0, group=None, out=None
     return None
 
 
+def gather_crcs_async(local, world: int, rank: int, out=None, dst: int = 0, group=None):
+    """gather_crcs for equal shards without waiting: returns the collective's work handle
+    (None when world == 1).  With "nccl" the gather runs on the collective's stream after
+    the work already queued on the current stream; `work.wait()` makes the current
+    stream wait for it, so `local` may be overwritten and `out` (required on `dst`, in
+    the tensors' device memory) read after that.  A caller can so overlap the gather of
+    one batch's results with the next batch's CRC launch.  With "gloo" the tensors must
+    be host tensors.  A one-rank world gathers to itself (same code path)."""
+    import torch.distributed as dist
+
+    if rank == dst:
+        if out is None or out.numel() != world * local.numel():
+            raise ValueError(f"dst needs out with {world} x {local.numel()} elements")
+        return dist.gather(local, gather_list=list(out.view(world, -1).unbind(0)), dst=dst, group=group, async_op=True)
+    return dist.gather(local, gather_list=None, dst=dst, group=group, async_op=True)
+
+
 def gather_crcs_var(local, counts, rank: int, dst: int = 0, group=None):
     """Gather per-rank CRC tensors of different lengths (the byte-balanced partition of
     a mixed-length batch, shard_by_bytes) to `dst`.  `counts[r]` = rank r's packet

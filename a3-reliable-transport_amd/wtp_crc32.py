@@ -39,6 +39,7 @@ def _load() -> C.CDLL:
         "wtp_device_count": (i32, []),
         "wtp_init": (i32, [i32]),
         "wtp_device_status": (i32, [i32, C.POINTER(u32), i32]),
+        "wtp_reserve_cus": (i32, [i32, i32]),
         "wtp_crc32": (u32, [vp, sz]),
         "wtp_crc32_batch_fixed": (i32, [vp, sz, sz, sz, vp, vp]),
         "wtp_crc32_batch_var": (i32, [vp, sz, vp, vp, sz, vp, vp]),
@@ -61,7 +62,7 @@ def _load() -> C.CDLL:
 
 
 LIB = _load()
-EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_crc32",
+EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_reserve_cus", "wtp_crc32",
             "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_batch_packed", "wtp_crc32_verify_batch", "wtp_build_data_packets",
             "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify", "wtp_host_alloc",
             "wtp_host_free", "wtp_synth_fill")
@@ -130,6 +131,11 @@ def build_data_packets(payloads, total_bytes: int, seq0: int, wire, wire_stride:
 def synth_fill(out, start_byte: int = 0, seed: int = 0x5EED, nbytes: int | None = None, stream=None) -> None:
     nb = out.numel() * out.element_size() if nbytes is None else nbytes
     _check(LIB.wtp_synth_fill(_dptr(out), start_byte, nb, seed, _stream(stream)), "wtp_synth_fill")
+
+
+def reserve_cus(ncus: int, device: int = 0) -> None:
+    """Leave ncus CUs free of the library's persistent kernels (see wtp_reserve_cus)."""
+    _check(LIB.wtp_reserve_cus(device, ncus), "wtp_reserve_cus")
 
 
 def device_status(device: int = 0, clear: bool = True) -> int:

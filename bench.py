@@ -50,6 +50,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL gather inside the step")
+    ap.add_argument("--reserve-cus", type=int, default=None,
+                    help="CUs the CRC kernel leaves free (wtp_reserve_cus); default 8 with the gather "
+                         "(for the overlapped RCCL gather's workgroups), else 0")
+    ap.add_argument("--gather-n1", action="store_true",
+                    help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box read-ceiling probe")
     return ap.parse_args()
 
@@ -234,7 +239,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
-    if world > 1:
+    if world > 1 or args.gather_n1:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                s = socket.socket()
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+                s.close()
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -248,25 +263,66 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     if W.LIB.wtp_init(torch.cuda.current_device()) != 0:
         raise W.WtpError(W.LIB.wtp_last_error().decode())
-    stream = torch.cuda.current_stream()
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
 
     # this rank's contiguous shard of the global packet stream, generated on-device
     buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
     W.synth_fill(buf, start_byte=rank * nbytes, seed=SEED, nbytes=nbytes)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
-    do_gather = world > 1 and not args.no_gather
+    do_gather = (world > 1 or args.gather_n1) and not args.no_gather
+    # with the gather, the CRC launches get a stream of their own (the collective's stream
+    # then syncs with it, not with the legacy default stream)
+    stream = torch.cuda.Stream() if do_gather else torch.cuda.current_stream()
+    torch.cuda.set_stream(stream)
+    reserve = args.reserve_cus if args.reserve_cus is not None else (8 if do_gather else 0)
+    if reserve:
+        W.reserve_cus(reserve, torch.cuda.current_device())
     gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
+
+    class Pipe:
+        """Step i: the CRC of this rank's shard into outs[i % 2] on `stream`, then (N > 1)
+        the RCCL gather of those results to rank 0, asynchronous: it runs on the
+        collective's stream, on the CUs the CRC kernel leaves free (wtp_reserve_cus),
+        while step i+1's CRC runs; outs[b] is rewritten only after its gather is done."""
+
+        def __init__(self):
+            self.outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2 if do_gather else 1)]
+            self.works = [None] * len(self.outs)
+            self.i = 0
+
+        def wait_slot(self):
+            b = self.i % len(self.outs)
+            if self.works[b] is not None:
+                self.works[b].wait()
+                self.works[b] = None
+
+        def launch(self):
+            W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, self.outs[self.i % len(self.outs)], stream)
+
+        def finish(self):
+            if do_gather:
+                b = self.i % 2
+                self.works[b] = shard.gather_crcs_async(self.outs[b], world, rank, out=gathered)
+            self.i += 1
+
+        def step(self):
+            self.wait_slot()
+            self.launch()
+            self.finish()
+
+        def drain(self):
+            for b, w in enumerate(self.works):
+                if w is not None:
+                    w.wait()
+                    self.works[b] = None
+
+    pipe = Pipe()
+    out = pipe.outs[0]
 
     def crc():
         W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
 
-    def step():
-        crc()
-        if do_gather:
-            shard.gather_crcs(out, world, rank, out=gathered)
-
-    warm_done, warm_means = settle(step, stream, args.warmup)
+    warm_done, warm_means = settle(pipe.step, stream, args.warmup)
+    pipe.drain()
     torch.cuda.synchronize()
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -276,11 +332,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        pipe.wait_slot()  # (stream-side) before the start event: it times the kernel alone
         starts[i].record(stream)
-        crc()
+        pipe.launch()
         ends[i].record(stream)
-        if do_gather:
-            shard.gather_crcs(out, world, rank, out=gathered)
+        pipe.finish()
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -298,7 +355,7 @@ def main():
     parity = None
     if rank == 0:
         import numpy as np
-        vec = (gathered if gathered is not None else out).cpu().numpy().view(np.uint32)
+        vec = (gathered if gathered is not None else pipe.outs[(args.steps - 1) % len(pipe.outs)]).cpu().numpy().view(np.uint32)
         parity = parity_digest(vec)
         if parity["match"] is None:  # no reference digest for this size: oracle spot check
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -327,7 +384,9 @@ def main():
         "config": {"workload": f"crc32 of {n} x {PAYLOAD}-B DATA payloads per GPU, device-resident"
                                + (" + RCCL gather of u32 results to rank 0" if do_gather else ""),
                    "packets_per_rank": n, "payload_bytes": PAYLOAD, "global_packets": n * world,
-                   "parallelism": f"packet shards x{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"packet shards x{world}" if world > 1 else "single GPU",
+                   "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
+                   "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(n),
                      "kernel": "k_fixed_braid<6>", "kernel_ms_mean": round(kmean, 5),
@@ -350,7 +409,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(65536, args.cpu_seconds, threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     if parity is not None and parity["match"] is False:

@@ -69,6 +69,14 @@ int wtp_device_count(void);
    lazily on first use).  Call before capturing a launch into a hipGraph. */
 int wtp_init(int device);
 
+/* Leave `ncus` compute units of `device` free of the library's persistent kernels
+   (0 <= ncus < the device's CUs; 0, the default, uses all).  For callers that overlap
+   RCCL collectives with CRC launches, e.g. the gather of one batch's results with the
+   next batch: a braided workgroup holds all of its CU's LDS, so a collective's
+   workgroups can only start on CUs the launch leaves free.  Affects later launches on
+   that device from any thread. */
+int wtp_reserve_cus(int device, int ncus);
+
 /* Sticky device-side data-error flags of `device` (bit 0: a general-kernel payload
    length was > WTP_MAX_KERNEL_LEN; that payload's result is then 0 / not ok).
    Synchronous; clears the flags when `clear` != 0. */

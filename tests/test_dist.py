@@ -6,6 +6,7 @@ HIP kernel (tests/test_gpu_shard.py) — and rank 0 compares the gathered vector
 the single-process result."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -162,3 +163,54 @@ def test_mixed_length_byte_shards_gather(world):
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     data = O.synth_fill_np(int(lens.sum()), start_byte=77)
     assert np.array_equal(got, O.batch_var(data, offs, lens))
+
+
+def _async_worker(rank, world, port, steps, q):
+    """Pipelined gather as bench.py runs it: step i writes slot i % 2, the gather of
+    step i is in flight while step i+1 is computed, a slot is rewritten only after its
+    gather was waited for.  Rank r's step-i values are r * 1000 + i * 7 + lane."""
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "..", "a3-reliable-transport_amd"))
+    import shard as S
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 257
+    outs = [torch.empty(n, dtype=torch.int32) for _ in range(2)]
+    works = [None, None]
+    gathered = [torch.empty(world * n, dtype=torch.int32) for _ in range(steps)] if rank == 0 else [None] * steps
+    for i in range(steps):
+        b = i % 2
+        if works[b] is not None:
+            works[b].wait()
+        outs[b].copy_(torch.arange(n, dtype=torch.int32) + rank * 1000 + i * 7)
+        works[b] = S.gather_crcs_async(outs[b], world, rank, out=gathered[i])
+    for w in works:
+        if w is not None:
+            w.wait()
+    if rank == 0:
+        q.put([g.numpy().copy() for g in gathered])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_gather_async_pipelined(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    steps = 5
+    procs = [ctx.Process(target=_async_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = 257
+    for i, g in enumerate(got):
+        want = np.concatenate([np.arange(n) + r * 1000 + i * 7 for r in range(world)]).astype(np.int32)
+        assert np.array_equal(g, want), i
