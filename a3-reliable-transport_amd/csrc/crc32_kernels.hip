@@ -1559,7 +1559,15 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
     const unsigned threads = BEpi::kCopy ? kBuildThreads : kBraidThreads;
     const uint64_t rounds = (n + 3) / 4;
     const uint64_t want = (rounds + threads / 64 - 1) / (threads / 64);
-    const unsigned grid = unsigned(want < uint64_t(s.grid_cus()) ? want : uint64_t(s.grid_cus()));
+    uint64_t cap = s.grid_cus();
+    // Long streaming batches (>= 64 rounds per wave) run one workgroup per XCD fewer than
+    // CUs: fewer rows in flight queue less at HBM.  Interleaved A/B, 8 reps
+    // (profiles/r02h/ab_reserve2.log): 1 M x 1456 B 220.6 us at 256 workgroups, 218.7 at
+    // 252, 217.4 at 248, 217.5-217.7 at 244-232; 2 M 460.6 vs 452.2 us at 248.  Short
+    // batches keep every CU (C2: 8 rounds per wave, a ninth would be its tail).
+    if (!BEpi::kCopy && s.reserve.load(std::memory_order_relaxed) == 0 && rounds >= 64 * cap * (threads / 64))
+        cap -= cap / 32;
+    const unsigned grid = unsigned(want < cap ? want : cap);
     epi.cinit = init_const(len);
     switch (rows) {
         case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
