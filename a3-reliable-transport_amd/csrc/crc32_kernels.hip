@@ -630,7 +630,9 @@ constexpr uint32_t kPcChunks = 272;  // span chunks a slot holds: 64 pieces + ga
 constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read one chunk past
 constexpr uint32_t kPcFlags = kPcStage + 16 * kPcSlot;  // 64 B per wave: packet-start flags
 constexpr uint32_t kPcBal = kPcFlags + 16 * 64;          // wave split: 16 piece sums, 17 u64 starts
-constexpr uint32_t kPcLdsWords = (kPcBal + 64 + 17 * 8) / 4;  // 161,752 B
+constexpr uint32_t kPcSpre = kPcBal + 64 + 17 * 8;       // 17 u32: pieces before each wave's range
+constexpr uint32_t kPcRem = kPcSpre + 80;                // 16 u32: pieces each wave has left, by SIMD
+constexpr uint32_t kPcLdsWords = (kPcRem + 64) / 4;      // 161,896 B
 static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
 static_assert(kPcLdsWords * 4 <= 163840, "LDS");
 
@@ -679,6 +681,9 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 #define WTP_PC_THREADS 1024
 #endif
 constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThreads);
+#ifndef WTP_PC_LAG
+#define WTP_PC_LAG 1  // k_pieces: wave priority by work left (0: rotate by round and age)
+#endif
 static_assert(kPcThreads >= 128 && kPcThreads <= 1024 && (kPcThreads & (kPcThreads - 1)) == 0, "k_pieces block");
 struct WaveSplit {
     static constexpr uint32_t kReg = 8, kThreads = kPcThreads, kWaves = kThreads / 64;
@@ -693,8 +698,8 @@ struct WaveSplit {
         for (uint32_t j = 0; j < kReg; ++j) raw[j] = prov.load_len(a + j < b ? a + j : g0);  // g0 < g1: valid
     }
     template <class Prov>
-    __device__ __forceinline__ void finish(const Prov &prov, uint64_t g0, uint64_t g1,
-                                           char *lds, uint32_t wave, uint32_t lane, uint64_t &lo, uint64_t &hi) {
+    __device__ __forceinline__ void finish(const Prov &prov, uint64_t g0, uint64_t g1, char *lds, uint32_t wave,
+                                           uint32_t lane, uint64_t &lo, uint64_t &hi, uint32_t &wpieces) {
         constexpr uint32_t nw = kWaves;
         const uint64_t m = b - a;
         uint32_t k[kReg], sum = 0;
@@ -707,10 +712,12 @@ struct WaveSplit {
         const uint32_t incl = wave_incl_add(sum);
         uint32_t *const wsum = reinterpret_cast<uint32_t *>(lds + kPcBal);
         uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kPcBal + 64);
+        uint32_t *const spre = reinterpret_cast<uint32_t *>(lds + kPcSpre);
         if (lane == 63u) wsum[wave] = incl;
         if (threadIdx.x == 0) {
             starts[0] = g0;
             starts[nw] = g1;
+            spre[0] = 0;
         }
         __syncthreads();
         uint32_t before = 0, total = 0;
@@ -733,11 +740,14 @@ struct WaveSplit {
                 }
                 while (p < b && pre < target) pre += piece_count(prov, p++);
                 starts[w] = p;
+                spre[w] = pre;
             }
         }
+        if (threadIdx.x == 0) spre[nw] = total;
         __syncthreads();
         lo = uniform64(starts[wave]);
         hi = uniform64(starts[wave + 1]);
+        wpieces = uint32_t(__builtin_amdgcn_readfirstlane(int(spre[wave + 1] - spre[wave])));
     }
 };
 
@@ -823,8 +833,9 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
         if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = hv;
     }
     uint64_t lo, hi;
+    uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
     if constexpr (Prov::kVarLen) {
-        split.finish(prov, g0, g1, lds, wave, lane, lo, hi);  // its barriers also publish the tables
+        split.finish(prov, g0, g1, lds, wave, lane, lo, hi, wpieces);  // its barriers also publish the tables
     } else {
         lo = n * (w0 + wave) / tw;
         hi = n * (w0 + wave + 1) / tw;
@@ -852,7 +863,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     uint32_t skip = 0, carry = 0;  // pieces of packet p0 done in earlier rounds, their register
     int32_t spec = kNoSpan;        // view offset of the prefetched span
     u32x4 x[5];
-    uint32_t nrounds = 0;
+    uint32_t nrounds = 0, done = 0;
     for (uint64_t p0 = lo; p0 < hi;) {
         uint64_t off;
         uint32_t len, aux = 0, oslot = 0;
@@ -994,7 +1005,21 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
         skip = partial ? last_gp + 1 : 0u;
         p0 = p0n;
         if (WTP_PROBE && nrounds == 0) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
-        rotate_prio(++nrounds + (wave >> 2));
+        ++nrounds;
+        if constexpr (Prov::kVarLen && WTP_PC_LAG) {
+            // The SIMD arbiter serves the oldest of equal-priority waves first, so with a
+            // fixed rotation the youngest waves still ended ~8 us after the oldest
+            // (tools/pprobe.py).  Priority = how many of the SIMD's four waves have less
+            // work left than this one (stale reads only blur the ranking).
+            done += total;
+            const uint32_t left = wpieces > done ? wpieces - done : 0u;
+            const uint32_t simd = wave & 3u;
+            if (lane == 0) lds_w[kPcRem / 4 + 4u * simd + (wave >> 2)] = left;
+            const u32x4 r4 = *(const lu32x4 *)((lchar *)lds_w + kPcRem + 16u * simd);
+            rotate_prio(uint32_t(r4.x < left) + uint32_t(r4.y < left) + uint32_t(r4.z < left) + uint32_t(r4.w < left));
+        } else {
+            rotate_prio(nrounds + (wave >> 2));
+        }
     }
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     PC_PROBE(6, nrounds);
