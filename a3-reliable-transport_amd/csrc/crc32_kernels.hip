@@ -681,6 +681,9 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 #define WTP_PC_THREADS 1024
 #endif
 constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThreads);
+#ifndef WTP_PC_LEN128
+#define WTP_PC_LEN128 1  // wave split: length words by two 16-B loads (0: eight dword loads)
+#endif
 #ifndef WTP_PC_LAG
 #define WTP_PC_LAG 1  // k_pieces: wave priority by work left (0: rotate by round and age)
 #endif
@@ -694,8 +697,20 @@ struct WaveSplit {
         const uint64_t R = g1 - g0;
         a = g0 + ((R * threadIdx.x) >> kPcLogT);
         b = g0 + ((R * (threadIdx.x + 1)) >> kPcLogT);
+#if WTP_PC_LEN128
+        // the sub-range's first 8 length words as two 16-B buffer loads (4-B aligned is
+        // enough; words at or past g1 read 0 and are never used): a quarter of the vector
+        // memory instructions of 8 dword loads, in the prologue where they queue behind
+        // the table loads
+        static_assert(kReg == 8, "two 16-B loads");
+        const __amdgpu_buffer_rsrc_t lr = make_rsrc(prov.len_array(), uint32_t(4 * g1));
+        const u32x4 l0 = buf_ld16(lr, uint32_t(4 * a)), l1 = buf_ld16(lr, uint32_t(4 * a + 16));
+        raw[0] = l0.x; raw[1] = l0.y; raw[2] = l0.z; raw[3] = l0.w;
+        raw[4] = l1.x; raw[5] = l1.y; raw[6] = l1.z; raw[7] = l1.w;
+#else
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) raw[j] = prov.load_len(a + j < b ? a + j : g0);  // g0 < g1: valid
+#endif
     }
     template <class Prov>
     __device__ __forceinline__ void finish(const Prov &prov, uint64_t g0, uint64_t g1, char *lds, uint32_t wave,
@@ -1675,6 +1690,7 @@ struct ArrayProvL {
         r.b = lens[p];
     }
     __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
+    __device__ __forceinline__ const uint32_t *len_array() const { return lens; }
     __device__ __forceinline__ uint32_t len_of(uint32_t w) const { return w; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
                                            uint32_t &) const {
@@ -1704,6 +1720,7 @@ struct DgramProvL {
         r.d = w.y;
     }
     __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return rl[p]; }
+    __device__ __forceinline__ const uint32_t *len_array() const { return rl; }
     __device__ __forceinline__ uint32_t len_of(uint32_t r) const { return r >= 16 && r <= stride ? r - 16 : 0u; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
                                            uint32_t &) const {
