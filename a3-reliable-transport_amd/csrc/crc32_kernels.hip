@@ -1916,11 +1916,14 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
         const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
         const uint64_t need = 2 + std::min<uint64_t>(per, n);
         // The fix-up list: the stream's persistent slot (zeroed once, reset by the fix-up
-        // pass), or, while the stream is being captured into a graph (whose replays need
-        // not follow this stream's order), scratch of this call zeroed by a memset node.
+        // pass), or scratch of this call zeroed by a memset node while the stream is being
+        // captured into a graph (whose replays need not follow this stream's order) and
+        // for hipStreamPerThread (one handle, a different stream in every host thread).
+        // Slots are keyed by handle: a stream destroyed with a verify still in flight
+        // whose handle a new stream then reuses would share its slot with that verify.
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         WTP_HIP(hipStreamIsCapturing(st, &cs));
-        const bool scratch = cs != hipStreamCaptureStatusNone;
+        const bool scratch = cs != hipStreamCaptureStatusNone || st == hipStreamPerThread;
         std::unique_lock<std::mutex> lk(s->fix_mu, std::defer_lock);  // held until the launches are queued
         uint32_t *fix = nullptr;
         if (scratch) {

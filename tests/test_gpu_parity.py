@@ -616,6 +616,21 @@ def test_verify_fixup_slot_reuse(W):
         for n in (3001, 64):
             outs.append((n, *run(n)))
     torch.cuda.synchronize()
+    # hipStreamPerThread (handle 2): a different stream in every host thread, so it takes
+    # per-call scratch; two threads at once
+    import threading
+    res = {}
+
+    def per_thread(tag, n):
+        res[tag] = (n, *run(n, stream=2))
+
+    ths = [threading.Thread(target=per_thread, args=(t, n)) for t, n in (("a", 3001), ("b", 20000))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    outs.extend(res.values())
+    torch.cuda.synchronize()
     for n, ok, crc in outs:
         if n is None:
             assert bool(ok.all())
