@@ -1745,6 +1745,7 @@ struct IdxDgramProvL {
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
     uint32_t *fix;
+    uint32_t nidx;  // datagrams of the batch (>= 1): listed indices are clamped below it
     __device__ __forceinline__ uint64_t count(uint64_t n) const {
         const uint64_t c = *(const __attribute__((address_space(1))) uint32_t *)fix;  // written by the braid pass
         return c < n ? c : n;
@@ -1756,7 +1757,8 @@ struct IdxDgramProvL {
         }
     }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
-        const uint32_t idx = fix[2 + p];
+        const uint32_t i0 = fix[2 + p];
+        const uint32_t idx = i0 < nidx ? i0 : nidx - 1;  // a listed index is < nidx unless the slot was shared
         const uint32_t h = uint32_t(lead + uint64_t(idx) * stride + 12) & ~3u;
         r.a = idx;
         r.b = rl[idx];
@@ -1915,60 +1917,60 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
         const uint32_t flen = uint32_t(std::min<size_t>(stride - 16, WTP_MAX_PAYLOAD));
         const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
         const uint64_t need = 2 + std::min<uint64_t>(per, n);
-        // The fix-up list: the stream's persistent slot (zeroed once, reset by the fix-up
-        // pass), or scratch of this call zeroed by a memset node while the stream is being
-        // captured into a graph (whose replays need not follow this stream's order) and
-        // for hipStreamPerThread (one handle, a different stream in every host thread).
-        // Slots are keyed by handle: a stream destroyed with a verify still in flight
-        // whose handle a new stream then reuses would share its slot with that verify.
+        // The fix-up list is the stream's persistent slot: zeroed once when allocated,
+        // then reset by the fix-up pass itself.  No allocation ever happens inside a graph
+        // capture: a capture uses the capturing stream's slot if an earlier call on that
+        // stream made one large enough (the graph then shares it with the stream: replay
+        // it on that stream, or not concurrently with the stream's other verify calls);
+        // otherwise the call takes the general kernel below, which needs no list.  So does
+        // hipStreamPerThread (one handle, a different stream in every host thread).  Slots
+        // are keyed by handle: a stream destroyed with a verify still in flight whose
+        // handle a new stream then reuses would share its slot with that verify (the
+        // fix-up pass clamps every listed index to the batch, so a shared slot can give
+        // wrong results but never an out-of-bounds access).
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         WTP_HIP(hipStreamIsCapturing(st, &cs));
-        const bool scratch = cs != hipStreamCaptureStatusNone || st == hipStreamPerThread;
+        const bool capturing = cs != hipStreamCaptureStatusNone;
         std::unique_lock<std::mutex> lk(s->fix_mu, std::defer_lock);  // held until the launches are queued
         uint32_t *fix = nullptr;
-        if (scratch) {
-            WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&fix), 4 * need, s->pool, st));
-            if (hipMemsetAsync(fix, 0, 8, st) != hipSuccess) {
-                (void)hipFreeAsync(fix, st);
-                return fail(WTP_EHIP, "hipMemsetAsync failed");
-            }
-        } else {
+        if (st != hipStreamPerThread) {
             lk.lock();
-            DevState::FixSlot &slot = s->fix_slots[st];
-            if (slot.cap < need) {
-                if (slot.buf) WTP_HIP(hipFreeAsync(slot.buf, st));  // after the stream's earlier uses
-                slot.buf = nullptr;
-                slot.cap = 0;
-                uint32_t *nb = nullptr;
-                WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&nb), 4 * need, s->pool, st));
-                if (hipMemsetAsync(nb, 0, 8, st) != hipSuccess) {
-                    (void)hipFreeAsync(nb, st);
-                    return fail(WTP_EHIP, "hipMemsetAsync failed");
+            if (capturing) {
+                auto it = s->fix_slots.find(st);
+                if (it != s->fix_slots.end() && it->second.cap >= need) fix = it->second.buf;
+            } else {
+                DevState::FixSlot &slot = s->fix_slots[st];
+                if (slot.cap < need) {
+                    if (slot.buf) WTP_HIP(hipFreeAsync(slot.buf, st));  // after the stream's earlier uses
+                    slot.buf = nullptr;
+                    slot.cap = 0;
+                    uint32_t *nb = nullptr;
+                    WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&nb), 4 * need, s->pool, st));
+                    if (hipMemsetAsync(nb, 0, 8, st) != hipSuccess) {
+                        (void)hipFreeAsync(nb, st);
+                        return fail(WTP_EHIP, "hipMemsetAsync failed");
+                    }
+                    slot.buf = nb;
+                    slot.cap = need;
                 }
-                slot.buf = nb;
-                slot.cap = need;
+                fix = slot.buf;
             }
-            fix = slot.buf;
         }
-        for (uint64_t p = 0; p < n && !rc; p += per) {
-            const uint64_t cnt = std::min<uint64_t>(per, n - p);
-            const uint8_t *sb = b + p * stride;
-            uint8_t *ok = d_ok + p;
-            uint32_t *crc = d_crc_out ? d_crc_out + p : nullptr;
-            rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
-                                    dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt, 16u + flen}, st);
-            if (!rc)
-                rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix}, cnt,
-                                   dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);
+        if (fix) {
+            for (uint64_t p = 0; p < n && !rc; p += per) {
+                const uint64_t cnt = std::min<uint64_t>(per, n - p);
+                const uint8_t *sb = b + p * stride;
+                uint8_t *ok = d_ok + p;
+                uint32_t *crc = d_crc_out ? d_crc_out + p : nullptr;
+                rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
+                                        dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt, 16u + flen}, st);
+                if (!rc)
+                    rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix, uint32_t(cnt)}, cnt,
+                                       dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);
+            }
+            if (rc) (void)hipMemsetAsync(fix, 0, 8, st);  // a braid pass whose fix-up pass never ran left a count
+            return rc;
         }
-        if (scratch) {
-            const hipError_t fe = hipFreeAsync(fix, st);
-            if (rc) return rc;
-            if (fe != hipSuccess) return fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
-        } else if (rc) {
-            (void)hipMemsetAsync(fix, 0, 8, st);  // a braid pass whose fix-up pass never ran left a count
-        }
-        return rc;
     }
     const uint64_t per = std::min<uint64_t>(kSubBatch, std::max<uint64_t>(1, (1ull << 30) / stride));
     for (uint64_t p = 0; p < n; p += per) {

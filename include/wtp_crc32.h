@@ -129,7 +129,13 @@ int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t
    stride % 16 == 0 (e.g. 1472 = header + 1456, or wReceiver's 1504-B slots holding the
    reference's 1500-B receive buffer) runs the braided kernel over the first
    min(stride - 16, 1456) payload bytes of every slot, decides the datagrams of exactly
-   that length, and finishes the others in a second, general-kernel pass. */
+   that length, and finishes the others in a second, general-kernel pass.  That pass
+   reads a list of the others which the library keeps per (device, stream) for the
+   life of the process: no allocation or memset per call.  Captured into a graph, a call
+   uses the capturing stream's list if an earlier call on that stream created one (the
+   graph then shares it with that stream: replay it on that stream, or not concurrently
+   with the stream's other verify calls); otherwise, and on hipStreamPerThread, the
+   call runs the general kernel alone (no list, nothing allocated). */
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len,
                            size_t n, uint8_t *d_ok, uint32_t *d_crc_out, void *stream);
 

@@ -575,8 +575,9 @@ def test_verify_wreceiver_1504_slots(W, n):
 def test_verify_fixup_slot_reuse(W):
     """The fix-up list is a per-stream slot the fix-up pass resets itself: back-to-back
     calls on one stream (growing and shrinking batches), calls on a second stream, an
-    all-full ring (empty list) between them, and a CUDA-graph capture (per-call scratch)
-    replayed twice all stay bit-exact."""
+    all-full ring (empty list) between them, hipStreamPerThread from two threads (general
+    kernel), and CUDA-graph captures on a fresh stream (general kernel) and on a stream
+    with a slot (the slot), each replayed twice, all stay bit-exact."""
     rng = np.random.default_rng(2024)
     stride = 1504
     rings = {}
@@ -617,7 +618,7 @@ def test_verify_fixup_slot_reuse(W):
             outs.append((n, *run(n)))
     torch.cuda.synchronize()
     # hipStreamPerThread (handle 2): a different stream in every host thread, so it takes
-    # per-call scratch; two threads at once
+    # the general kernel (no list); two threads at once
     import threading
     res = {}
 
@@ -636,24 +637,30 @@ def test_verify_fixup_slot_reuse(W):
             assert bool(ok.all())
         else:
             check(n, ok, crc)
-    # graph capture: the fix-up list is scratch of the captured call, zeroed by the graph
+    # graph capture never allocates: on a fresh stream the captured call takes the
+    # general kernel (no list); on a stream with a slot it uses that slot
     d, r, _, _ = rings[3001]
-    gok = torch.full((3001,), 7, dtype=torch.uint8, device="cuda")
-    gcrc = u32_out(3001)
-    g = torch.cuda.CUDAGraph()
-    cs = torch.cuda.Stream()
-    cs.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(cs):
-        g.capture_begin()
-        W.verify_batch(d, stride, r, 3001, gok, gcrc)
-        g.capture_end()
-    torch.cuda.current_stream().wait_stream(cs)
-    for _ in range(2):
-        gok.fill_(7)
-        g.replay()
-        torch.cuda.synchronize()
-        check(3001, gok, gcrc)
-        check(97, *run(97))  # the stream's slot is untouched by the graph
+    for warm in (False, True):
+        gok = torch.full((3001,), 7, dtype=torch.uint8, device="cuda")
+        gcrc = u32_out(3001)
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            if warm:
+                run(3001, stream=cs)
+                cs.synchronize()
+            g.capture_begin()
+            W.verify_batch(d, stride, r, 3001, gok, gcrc)
+            g.capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
+        for _ in range(2):
+            gok.fill_(7)
+            with torch.cuda.stream(cs):
+                g.replay()
+            torch.cuda.synchronize()
+            check(3001, gok, gcrc)
+            check(97, *run(97))  # the default stream's slot is untouched by the graph
 
 
 def test_verify_misaligned_ring_takes_general_path(W):
