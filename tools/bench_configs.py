@@ -53,7 +53,14 @@ def graph_time(fn, G=50, reps=7, per=10):
     between kernels): median over `reps` timings of `per` consecutive replays (timing each
     replay on its own adds the graph-launch gap, ~1.7 us per launch at G = 50)."""
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # capture on a stream that ran fn once first: library state keyed by stream (the
+    # verify fix-up list) exists before the capture, which never allocates
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        fn()
+    cs.synchronize()
+    with torch.cuda.graph(graph, stream=cs):
         for _ in range(G):
             fn()
     for _ in range(2):
