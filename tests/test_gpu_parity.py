@@ -66,6 +66,44 @@ def test_golden_batch_digest(W, golden):
     assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_le_u32"]
 
 
+def test_reserve_cus_keeps_results(W, golden):
+    """wtp_reserve_cus shrinks the persistent grids; results stay bit-exact (golden
+    4096 x 1456 digest, a long batch past the 64-rounds-per-wave grid rule, and a mixed
+    batch through the general kernel), and out-of-range counts are rejected."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    g = golden["batch_4096x1456"]
+    buf = torch.empty(4096 * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    n2 = 600_000
+    big = torch.empty(n2 * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(big)
+    ref2 = None
+    lens = O.zipf_lengths(20_000, s=1.1)
+    try:
+        for r in (0, 8, cus // 2, cus - 1):
+            W.reserve_cus(r)
+            out = u32_out(4096)
+            W.crc32_batch_fixed(buf, 1456, 1456, 4096, out)
+            got = to_u32(out, 4096)
+            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_le_u32"], r
+            o2 = u32_out(n2)
+            W.crc32_batch_fixed(big, 1456, 1456, n2, o2)
+            v2 = to_u32(o2, n2).copy()
+            if ref2 is None:
+                ref2 = v2
+                idx = np.random.default_rng(5).choice(n2, 300, replace=False)
+                host = big.cpu().numpy()
+                for i in idx:
+                    assert v2[i] == O.crc32(host[i * 1456:(i + 1) * 1456]), i
+            assert np.array_equal(v2, ref2), r
+            _var_check(W.crc32_batch_var, lens, seed=r)
+        for bad in (-1, cus, cus + 5):
+            with pytest.raises(W.WtpError):
+                W.reserve_cus(bad)
+    finally:
+        W.reserve_cus(0)
+
+
 @pytest.mark.parametrize("L", [16, 240, 256, 272, 512, 1024, 1280, 1296, 1440, 1456, 1536])
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 257, 4099])
 def test_fast_path_lengths_and_tails(W, L, n):
