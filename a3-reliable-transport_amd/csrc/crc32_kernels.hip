@@ -1487,6 +1487,7 @@ struct DevState {
     std::unordered_map<hipStream_t, FixSlot> fix_slots;
 };
 constexpr int kMaxDev = 64;
+constexpr size_t kMaxFixSlots = 256;  // verify fix-up slots per device (one per stream used)
 DevState g_dev[kMaxDev];
 
 std::vector<uint32_t> host_tables() {
@@ -1939,6 +1940,13 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
                 auto it = s->fix_slots.find(st);
                 if (it != s->fix_slots.end() && it->second.cap >= need) fix = it->second.buf;
             } else {
+                if (s->fix_slots.size() >= kMaxFixSlots && !s->fix_slots.count(st)) {
+                    // bounded: a process that cycles through many streams (destroyed ones
+                    // keep their entries) drops every slot once the device is idle
+                    WTP_HIP(hipDeviceSynchronize());
+                    for (auto &kv : s->fix_slots) (void)hipFreeAsync(kv.second.buf, nullptr);  // device idle
+                    s->fix_slots.clear();
+                }
                 DevState::FixSlot &slot = s->fix_slots[st];
                 if (slot.cap < need) {
                     if (slot.buf) WTP_HIP(hipFreeAsync(slot.buf, st));  // after the stream's earlier uses

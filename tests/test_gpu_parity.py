@@ -701,6 +701,38 @@ def test_verify_fixup_slot_reuse(W):
             check(97, *run(97))  # the default stream's slot is untouched by the graph
 
 
+def test_verify_many_streams_slot_bound(W):
+    """More streams than the library keeps fix-up slots for (256 per device): the slots
+    are dropped and rebuilt; every call on every stream stays bit-exact."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    rng = np.random.default_rng(77)
+    n, stride = 97, 1504
+    buf, rl = _wtp_ring(n, stride, rng)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    d = dev_u8(buf)
+    r = torch.from_numpy(rl.view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    streams, outs = [], []
+    try:
+        for _ in range(300):
+            h = C.c_void_p()
+            assert hip.hipStreamCreate(C.byref(h)) == 0
+            streams.append(h)
+            ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            crc = u32_out(n)
+            W.verify_batch(d, stride, r, n, ok, crc, stream=h.value)
+            outs.append((ok, crc))
+        torch.cuda.synchronize()
+        for ok, crc in outs:
+            assert np.array_equal(ok.cpu().numpy(), want_ok)
+            assert np.array_equal(to_u32(crc, n), want_crc)
+    finally:
+        torch.cuda.synchronize()
+        for h in streams:
+            hip.hipStreamDestroy(h)
+
+
 def test_verify_misaligned_ring_takes_general_path(W):
     rng = np.random.default_rng(11)
     n, stride = 700, 1472
