@@ -138,3 +138,19 @@ def test_group_gather_all_devices(W, tmp_path):
     total = sum(n_per)
     want = O.batch_fixed(O.synth_fill_np(total * PAYLOAD), PAYLOAD, PAYLOAD, total, threads=THREADS)
     assert np.array_equal(got, want)
+
+
+def test_bench_pipelined_gather_one_rank(W):
+    """bench.py's N > 1 step (CRC on its own stream, asynchronous RCCL gather of the
+    results double-buffered behind the next launch, 8 reserved CUs) in a one-rank RCCL
+    world: the gathered vector's sha256 equals the reference digest for 1 M packets."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gather-n1", "--steps", "5", "--warmup", "5",
+                        "--no-cpu-baseline", "--no-probe"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["config"]["gather"] and line["config"]["reserved_cus"] == 8
+    assert line["parity"]["match"] is True, line["parity"]
