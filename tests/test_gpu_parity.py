@@ -191,9 +191,10 @@ def VAR(W, request):
     return W.crc32_batch_var if request.param == "var" else W.crc32_batch_packed
 
 
-@pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0)])
+@pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0), (1 << 20, 1.2)])
 def test_zipf_mixed_lengths(W, VAR, n, s):
-    """C5 itself at full size (1 M packets, Zipf 1.1 and 1.0), every packet vs the oracle."""
+    """C5 itself at full size (1 M packets, Zipf 1.1 and 1.0; 1.2, mean ~96 B, as SURVEY §8a
+    lists), every packet vs the oracle."""
     lens = O.zipf_lengths(n, s=s)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.sum())
@@ -731,6 +732,47 @@ def test_verify_many_streams_slot_bound(W):
         torch.cuda.synchronize()
         for h in streams:
             hip.hipStreamDestroy(h)
+
+
+def test_verify_sub_batches_share_the_slot(W):
+    """A ring longer than one fast-path launch takes (stride 16384: 131,071 datagrams per
+    sub-batch, the fix-up view < 2 GiB): two sub-batches reuse one fix-up slot, each
+    with short and corrupt datagrams of its own, including both sides of the boundary."""
+    stride, n = 16384, 140_000
+    per = ((1 << 31) - 4096) // stride
+    assert n > per
+    payload = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(payload, start_byte=99)
+    wire = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    wl = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)
+    del payload
+    rng = np.random.default_rng(140)
+    short = np.concatenate([rng.choice(per, 300, replace=False), per + rng.choice(n - per, 300, replace=False),
+                            [per - 1, per, per + 1]])
+    rl = wl.cpu().numpy().view(np.uint32).copy()
+    rl[short] = rng.integers(0, 1470, short.size).astype(np.uint32)
+    flip = np.concatenate([rng.choice(per, 50, replace=False), per + rng.choice(n - per, 50, replace=False)])
+    wv = wire.view(n, stride)
+    for i in flip:
+        wv[int(i), 100] ^= 0x20
+    r = torch.from_numpy(rl.view(np.int32)).cuda()
+    ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    crc = u32_out(n)
+    W.verify_batch(wire, stride, r, n, ok, crc)
+    got_ok = ok.cpu().numpy()
+    got_crc = to_u32(crc, n)
+    check = np.unique(np.concatenate([short, flip, rng.choice(n, 2000, replace=False), [0, n - 1]]))
+    for i in check:
+        i = int(i)
+        dg = wv[i].cpu().numpy()
+        want_ok, want_crc = O.verify_datagrams(dg, stride, rl[i:i + 1])
+        assert got_ok[i] == want_ok[0] and got_crc[i] == want_crc[0], i
+    # everything not shortened or flipped is a full, valid datagram
+    intact = np.ones(n, bool)
+    intact[short] = False
+    intact[flip] = False
+    assert got_ok[intact].all()
 
 
 def test_verify_misaligned_ring_takes_general_path(W):
