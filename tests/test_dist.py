@@ -214,3 +214,12 @@ def test_gather_async_pipelined(world):
     for i, g in enumerate(got):
         want = np.concatenate([np.arange(n) + r * 1000 + i * 7 for r in range(world)]).astype(np.int32)
         assert np.array_equal(g, want), i
+
+
+def test_gather_async_requires_out_on_dst():
+    """The asynchronous gather has no allocation path: dst must pass `out` of world x n."""
+    import torch
+    with pytest.raises(ValueError):
+        shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=None)
+    with pytest.raises(ValueError):
+        shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=torch.zeros(7, dtype=torch.int32))
