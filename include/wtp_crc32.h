@@ -105,16 +105,18 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
 int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                         const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
-/* The stream kernel explicitly, for mixed lengths stored back to back (a receive
-   buffer, a record file): d_offsets[i+1] == d_offsets[i] + d_lengths[i] (offsets =
-   exclusive prefix sum of the lengths, any first offset).  Each wave hashes its region
+/* Mixed lengths stored back to back (a receive buffer, a record file):
+   d_offsets[i+1] == d_offsets[i] + d_lengths[i] (offsets = exclusive prefix sum of the
+   lengths, any first offset).  The stream kernel: each wave hashes its region
    of the byte stream once and reads every payload's CRC off prefix values (no per-
    payload windows, masks or padding).  No limit on base_bytes (64-bit offsets) or n.
    Payloads that break the packing, or are longer than 4095 B, are still computed
    exactly on a slower lane-per-payload path, so results are correct for any offsets;
    lengths > WTP_MAX_KERNEL_LEN give crc 0 and set the status flag.
-   wtp_crc32_batch_var uses this kernel by itself for buffers >= 2 GiB; below that the
-   general kernel is currently the faster one on packed batches too (C5: DESIGN.md). */
+   The library picks the kernel: below 2 GiB the general kernel, currently the faster
+   one on packed batches too (C5: DESIGN.md), so this call then equals
+   wtp_crc32_batch_var; at or above 2 GiB the stream kernel (which wtp_crc32_batch_var
+   also uses there).  WTP_STREAM_KERNEL=1 in the environment forces the stream kernel. */
 int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 

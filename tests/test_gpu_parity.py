@@ -183,12 +183,23 @@ def test_general_strides_and_alignment(W, L, stride, lead):
     assert np.array_equal(to_u32(out, n), want)
 
 
-# Mixed-length tests run through both mixed-length entry points: wtp_crc32_batch_var
-# (k_pieces, any offsets) and wtp_crc32_batch_packed (k_stream; payloads that break the
+# Mixed-length tests run through every mixed-length route: wtp_crc32_batch_var
+# (k_pieces, any offsets), wtp_crc32_batch_packed (the same kernel below 2 GiB) and
+# wtp_crc32_batch_packed with WTP_STREAM_KERNEL=1 (k_stream; payloads that break the
 # packing take its lane-per-payload path, so every case must still be exact).
-@pytest.fixture(params=["var", "packed"])
+def _forced_stream(W):
+    def call(*a, **k):
+        os.environ["WTP_STREAM_KERNEL"] = "1"
+        try:
+            return W.crc32_batch_packed(*a, **k)
+        finally:
+            del os.environ["WTP_STREAM_KERNEL"]
+    return call
+
+
+@pytest.fixture(params=["var", "packed", "stream"])
 def VAR(W, request):
-    return W.crc32_batch_var if request.param == "var" else W.crc32_batch_packed
+    return {"var": W.crc32_batch_var, "packed": W.crc32_batch_packed, "stream": _forced_stream(W)}[request.param]
 
 
 @pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0), (1 << 20, 1.2)])

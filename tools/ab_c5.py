@@ -3,7 +3,9 @@
 a3-reliable-transport_amd/lib/ab/*.so, in one process on one box: each library is loaded
 with ctypes (RTLD_LOCAL: separate device state), the same Zipf batch is timed
 alternately (A B C ... A B C ...), and every library's output must equal the first's.
-  python tools/ab_c5.py [--s 1.1] [--reps 5]"""
+  python tools/ab_c5.py [--s 1.1] [--reps 5] [--entry var|packed]
+(--entry packed reaches the stream kernel only with WTP_STREAM_KERNEL=1 in the
+environment; below 2 GiB wtp_crc32_batch_packed otherwise takes the piece kernel)"""
 import argparse
 import ctypes as C
 import glob

@@ -151,9 +151,10 @@ def c3():
     return res
 
 
-def c5(s, entry="packed"):
-    """entry "packed": wtp_crc32_batch_packed (k_stream, the C5 layout: payloads back to
-    back); "var": wtp_crc32_batch_var (k_pieces, any offsets)."""
+def c5(s, entry="var"):
+    """entry "var": wtp_crc32_batch_var (k_pieces, any offsets); "packed":
+    wtp_crc32_batch_packed (the C5 layout, payloads back to back: the same k_pieces route
+    below 2 GiB); "stream": wtp_crc32_batch_packed with WTP_STREAM_KERNEL=1 (k_stream)."""
     n = 1 << 20
     lens = O.zipf_lengths(n, s=s)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
@@ -163,7 +164,9 @@ def c5(s, entry="packed"):
     do = torch.from_numpy(offs.view(np.int64)).cuda()
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.empty(n, dtype=torch.int32, device="cuda")
-    fn = W.crc32_batch_packed if entry == "packed" else W.crc32_batch_var
+    if entry == "stream":  # the stream kernel, forced (wtp_crc32_batch_packed picks k_pieces below 2 GiB)
+        os.environ["WTP_STREAM_KERNEL"] = "1"
+    fn = W.crc32_batch_packed if entry in ("packed", "stream") else W.crc32_batch_var
     f = lambda: fn(d, total, do, dl, n, out)  # noqa: E731
     med, mean = timed(f, 200)
     gl, _ = graph_time(f)
@@ -171,7 +174,9 @@ def c5(s, entry="packed"):
     host = d[:total].cpu().numpy()
     ok = bool(np.array_equal(got, O.batch_var(host, offs, lens)))
     rb = total + 12 * n
-    kern = "k_stream (wtp_crc32_batch_packed)" if entry == "packed" else "k_pieces (wtp_crc32_batch_var)"
+    os.environ.pop("WTP_STREAM_KERNEL", None)
+    kern = {"stream": "k_stream (wtp_crc32_batch_packed, WTP_STREAM_KERNEL=1)",
+            "packed": "wtp_crc32_batch_packed (k_pieces below 2 GiB)"}.get(entry, "k_pieces (wtp_crc32_batch_var)")
     return {"config": f"C5 1M mixed lengths Zipf(s={s}) on [1,1456], {kern}", "packets": n,
             "payload_bytes": total, "mean_len": round(total / n, 1), "read_bytes_incl_meta": rb,
             "ms_per_launch": round(mean, 4), "payload_GiBps": round(total / (mean * 1e-3) / GIB, 1),
@@ -238,7 +243,7 @@ def main():
     if "c2" in sel:
         res["results"].append(c2())
     if "c5" in sel:
-        for entry in ("packed", "var"):
+        for entry in ("stream", "var", "packed"):
             res["results"].append(c5(1.1, entry))
             res["results"].append(c5(1.0, entry))
     if "verify" in sel:
