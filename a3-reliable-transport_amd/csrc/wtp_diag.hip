@@ -75,4 +75,32 @@ int wtp_diag_clock(uint64_t *d_out, uint32_t iters, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Timing-only events (hip_runtime_api.h, hipEventDisableSystemFence: "for events that are
+// only being used to measure timing ... avoiding the cost of cache writeback and
+// invalidation, and the performance impact of those actions on the execution of
+// following work").
+int wtp_diag_event_create(void **ev) {
+    if (!ev) return -1;
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return -2;
+    *ev = e;
+    return 0;
+}
+
+int wtp_diag_event_record(void *ev, void *stream) {
+    if (!ev) return -1;
+    return hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -2;
+}
+
+int wtp_diag_event_elapsed_ms(void *start, void *end, float *ms) {
+    if (!start || !end || !ms) return -1;
+    if (hipEventSynchronize(static_cast<hipEvent_t>(end)) != hipSuccess) return -2;
+    return hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(end)) == hipSuccess ? 0 : -2;
+}
+
+int wtp_diag_event_destroy(void *ev) {
+    if (!ev) return 0;
+    return hipEventDestroy(static_cast<hipEvent_t>(ev)) == hipSuccess ? 0 : -2;
+}
+
 }  // extern "C"

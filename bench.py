@@ -173,20 +173,64 @@ def settle(step, stream, w_req: int, block: int = 25, tol: float = 0.01, floor: 
     return done, [round(m, 1) for m in means]
 
 
+_DIAG = None
+
+
+def diag():
+    """lib/libwtp_diag.so (include/wtp_diag.h): the read probe and timing-only events."""
+    global _DIAG
+    if _DIAG is None:
+        import ctypes as C
+        D = C.CDLL(os.path.join(PKG, "lib", "libwtp_diag.so"))
+        D.wtp_diag_read_xor.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint, C.c_uint, C.c_void_p]
+        D.wtp_diag_event_create.argtypes = [C.POINTER(C.c_void_p)]
+        D.wtp_diag_event_record.argtypes = [C.c_void_p, C.c_void_p]
+        D.wtp_diag_event_elapsed_ms.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]
+        D.wtp_diag_event_destroy.argtypes = [C.c_void_p]
+        _DIAG = D
+    return _DIAG
+
+
+class TimingEvent:
+    """A HIP event for timing only (hipEventDisableSystemFence, via libwtp_diag): recording
+    it does no system-scope cache writeback/invalidate, which the default event does and
+    which both pads the measured interval and slows the next launch."""
+
+    def __init__(self):
+        import ctypes as C
+        self._C = C
+        self.e = C.c_void_p()
+        if diag().wtp_diag_event_create(C.byref(self.e)) != 0:
+            raise RuntimeError("wtp_diag_event_create failed")
+
+    def record(self, stream):
+        if diag().wtp_diag_event_record(self.e, self._C.c_void_p(stream.cuda_stream)) != 0:
+            raise RuntimeError("wtp_diag_event_record failed")
+
+    def elapsed_time(self, end) -> float:
+        ms = self._C.c_float()
+        if diag().wtp_diag_event_elapsed_ms(self.e, end.e, self._C.byref(ms)) != 0:
+            raise RuntimeError("wtp_diag_event_elapsed_ms failed")
+        return ms.value
+
+    def __del__(self):
+        try:
+            diag().wtp_diag_event_destroy(self.e)
+        except Exception:
+            pass
+
+
 def read_ceiling(buf, nbytes: int, crc_step, stream, cus: int, reps: int = 10) -> dict:
     """Same-box HBM read ceiling: a plain nt dwordx4 streaming read + XOR over the same
     bytes (lib/libwtp_diag.so), timed interleaved with the CRC kernel."""
-    import ctypes as C
-
     import torch
 
-    D = C.CDLL(os.path.join(PKG, "lib", "libwtp_diag.so"))
-    D.wtp_diag_read_xor.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint, C.c_uint, C.c_void_p]
+    D = diag()
     sink = torch.zeros(4, dtype=torch.int32, device=buf.device)
     pe, ce = [], []
 
     def ev():
-        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        return TimingEvent(), TimingEvent()
 
     for i in range(reps + 2):
         s, e = ev()
@@ -325,8 +369,8 @@ def main():
     pipe.drain()
     torch.cuda.synchronize()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    starts = [TimingEvent() for _ in range(args.steps)]
+    ends = [TimingEvent() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

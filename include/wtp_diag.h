@@ -25,6 +25,14 @@ int wtp_diag_read_xor(const void *d_buf, size_t nbytes, uint32_t *d_sink, unsign
    (s_memtime), d_out[1] = 100 MHz ticks (s_memrealtime) over the spin. */
 int wtp_diag_clock(uint64_t *d_out, uint32_t iters, void *stream);
 
+/* Timing-only HIP events (created with hipEventDisableSystemFence: no system-scope cache
+   writeback/invalidate when recorded, so they perturb and pad the timed kernels least).
+   elapsed_ms waits for `end`.  0 on success, < 0 on failure. */
+int wtp_diag_event_create(void **ev);
+int wtp_diag_event_record(void *ev, void *stream);
+int wtp_diag_event_elapsed_ms(void *start, void *end, float *ms);
+int wtp_diag_event_destroy(void *ev);
+
 #ifdef __cplusplus
 }
 #endif
