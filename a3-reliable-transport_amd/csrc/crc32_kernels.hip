@@ -268,6 +268,7 @@ __device__ __forceinline__ void rotate_prio(uint32_t x) {
 // group ahead, the loads put() will need (so a flush never waits on memory).
 struct CrcBEpi {  // out[p] = crc
     static constexpr bool kCopy = false;  // see BuildBEpi
+    static constexpr int kBound = 1024;   // __launch_bounds__ (launched at 512; kbench A/B builds at up to 1024)
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
     struct Pre {};
@@ -284,6 +285,7 @@ struct CrcBEpi {  // out[p] = crc
 // list, which the general kernel finishes.
 struct VerifyBEpi {
     static constexpr bool kCopy = false;
+    static constexpr int kBound = 1024;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
     uint64_t stride;
@@ -323,6 +325,10 @@ struct VerifyBEpi {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes);
 struct BuildBEpi {
     static constexpr bool kCopy = true;
+    // launched at 128 threads: the bound lets the copy rows keep their registers (at the
+    // generic 1024 bound the compiler had 128 VGPRs and spilled 192-240 of them, 484 B of
+    // scratch per lane)
+    static constexpr int kBound = 128;
     uint8_t *wire;
     uint64_t wstride;  // multiple of 16
     uint32_t seq0, len;
@@ -387,7 +393,7 @@ struct BuildBEpi {
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
 // XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation.  Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
-__global__ __launch_bounds__(1024) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
+__global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
                                                       const uint32_t *__restrict__ gtab) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];

@@ -104,13 +104,17 @@ void stage_copy(void *dst, const void *src, size_t bytes) {
         memcpy(dst, src, bytes);
         return;
     }
-    const size_t per = ((bytes / parts) + 4095) & ~size_t(4095);
+    // ceil(bytes / parts) rounded up to a page, so parts * per >= bytes and the last part
+    // copies whatever is left (rounding floor(bytes / parts) up left bytes % parts bytes
+    // uncopied whenever floor(bytes / parts) was already page-aligned)
+    const size_t per = ((bytes + parts - 1) / parts + 4095) & ~size_t(4095);
     std::vector<std::thread> th;
     th.reserve(parts - 1);
     for (size_t i = 1; i < parts; ++i) {
         const size_t o = i * per;
         if (o >= bytes) break;
-        th.emplace_back([=] { memcpy(static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o, std::min(per, bytes - o)); });
+        const size_t cnt = i + 1 == parts ? bytes - o : std::min(per, bytes - o);
+        th.emplace_back([=] { memcpy(static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o, cnt); });
     }
     memcpy(dst, src, std::min(per, bytes));
     for (auto &t : th) t.join();

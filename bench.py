@@ -3,9 +3,10 @@
 
 One "step" = one pass of the hot path over one batch of synthetic, device-resident
 1456-byte DATA payloads: the braided CRC kernel over this rank's shard, plus (N > 1)
-the RCCL gather of the 32-bit results to rank 0.  Weak scaling: every rank owns
---packets-per-rank packets (default 1 M = the north-star 1 M x 1456 target at N = 1;
---packets-per-rank 2097152 at N = 8 is config C4, 16 M packets).
+the RCCL gather of the 32-bit results to rank 0.  Default shard sizes
+(default_packets_per_rank): N = 1 runs the metric's own workload, 1 M x 1456 B; N > 1
+runs config C4's per-GPU shard, 2 M x 1456 B per rank, so that N = 8 is exactly C4
+(16 M packets over 8 GPUs) and N = 2, 4 are the same per-rank work (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -44,10 +45,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5, help="minimum untimed launches (see settle())")
-    ap.add_argument("--packets-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--packets-per-rank", type=int, default=None,
+                    help="default: 1 M at N = 1 (the metric), 2 M at N > 1 (config C4's shard; N = 8 is C4)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="target wall seconds of the 1-thread CPU-baseline leg (the all-thread leg runs 1/3 of it)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every core this job may run on (sched_getaffinity, capped by a cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL gather inside the step")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -56,10 +59,57 @@ def parse():
     ap.add_argument("--gather-n1", action="store_true",
                     help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box read-ceiling probe")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.packets_per_rank is None:
+        a.packets_per_rank = default_packets_per_rank(a.gpus)
+    return a
 
 
-def cpu_baseline(n_sample: int, seconds: float, threads: int) -> dict:
+C4_PACKETS = 16 << 20  # BASELINE.json configs[3]: 16 M x 1456 B over 8 GPUs
+
+
+def default_packets_per_rank(gpus: int) -> int:
+    """N = 1: the metric's 1 M x 1456 B.  N > 1: C4's per-GPU shard (16 M / 8 = 2 M), so
+    the driver's plain `--gpus 8` run is config C4 and N = 2, 4 keep the same per-rank work."""
+    return 1 << 20 if gpus <= 1 else C4_PACKETS // 8
+
+
+def workload_name(world: int, n: int) -> str:
+    if world == 1 and n == 1 << 20:
+        return "target: 1 M x 1456 B on 1 GPU (BASELINE metric)"
+    if world * n == C4_PACKETS and world == 8:
+        return "C4: 16 M x 1456 B sharded over 8 GPUs + RCCL gather of the u32 results"
+    if n == C4_PACKETS // 8:
+        return f"C4 per-GPU shard (2 M x 1456 B) on {world} GPU(s)"
+    return f"{n} x 1456 B per GPU on {world} GPU(s)"
+
+
+def host_cores() -> dict:
+    """Cores this job may run on: the affinity mask, capped by a cgroup v2 CPU quota if
+    one is set (a 16-CPU share of a 256-core host shows all 256 in os.cpu_count()), and
+    the CPU model from /proc/cpuinfo."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"threads": use, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count(),
+            "model": model}
+
+
+def cpu_baseline(n_sample: int, seconds: float, threads: int, hc: dict | None = None) -> dict:
     """Reference crc32 (oracle/_ref) or, if it was not built, the oracle port."""
     import ctypes as C
 
@@ -111,6 +161,9 @@ def cpu_baseline(n_sample: int, seconds: float, threads: int) -> dict:
     assert zlib.crc32(mv[:PAYLOAD]) == int(out[0])
     return {
         "value": round(vn[0], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "cpu_model": (hc or {}).get("model"),
+        "cores_rule": "every CPU in this job's affinity mask, capped by its cgroup CPU quota" if hc else "--cpu-threads",
+        "host": hc,
         "sample": f"{n_sample} x {PAYLOAD} B synthetic packets (seed 0x5EED), looped ~{seconds:.0f} s on 1 thread and ~{seconds/3:.0f} s on {threads}; "
                   f"{kind} = {'cpp/src/common/Crc32.hpp:91-102 compiled -O2 (oracle/_ref)' if ref else 'oracle/crc32_oracle.c'}",
         "value_1core": round(v1[0], 4),
@@ -425,8 +478,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 seed 0x5EED, generated on-device per rank shard)",
-        "config": {"workload": f"crc32 of {n} x {PAYLOAD}-B DATA payloads per GPU, device-resident"
-                               + (" + RCCL gather of u32 results to rank 0" if do_gather else ""),
+        "config": {"workload": workload_name(world, n),
+                   "step": f"crc32 of {n} x {PAYLOAD}-B DATA payloads per GPU, device-resident"
+                           + (" + RCCL gather of u32 results to rank 0" if do_gather else ""),
                    "packets_per_rank": n, "payload_bytes": PAYLOAD, "global_packets": n * world,
                    "parallelism": f"packet shards x{world}" if world > 1 else "single GPU",
                    "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
@@ -449,8 +503,9 @@ def main():
         "parity": parity,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(65536, args.cpu_seconds, threads)
+        hc = host_cores()
+        threads = args.cpu_threads or hc["threads"]
+        line["cpu_baseline"] = cpu_baseline(65536, args.cpu_seconds, threads, hc)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

@@ -48,3 +48,29 @@ def test_parity_digest_lookup():
     assert p["match"] is None
     p = bench.parity_digest(np.zeros(1 << 20, np.uint32))
     assert p["match"] is False
+
+
+def test_default_shard_sizes_make_gpus8_config_c4(monkeypatch):
+    """The driver runs `bench.py --gpus N` with no other size flag; the self-launched
+    ranks re-parse the same argv.  N = 1 must be the metric's 1 M x 1456 B, N = 8 must be
+    config C4 (16 M x 1456 B = 2 M per rank), N = 2, 4 the same per-rank work."""
+    import bench
+    for gpus, ppr in ((1, 1 << 20), (2, 2 << 20), (4, 2 << 20), (8, 2 << 20)):
+        monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", str(gpus), "--steps", "5", "--warmup", "5"])
+        a = bench.parse()
+        assert a.packets_per_rank == ppr == bench.default_packets_per_rank(gpus)
+    assert 8 * bench.default_packets_per_rank(8) == 16777216
+    assert bench.workload_name(8, 2 << 20).startswith("C4: 16 M")
+    assert bench.workload_name(1, 1 << 20).startswith("target")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--packets-per-rank", "1000"])
+    assert bench.parse().packets_per_rank == 1000
+    # the reference digest for the gathered C4 vector exists
+    with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as f:
+        assert str(16777216) in json.load(f)["sha256_by_packets"]
+
+
+def test_host_cores_reports_affinity_and_model():
+    import bench
+    hc = bench.host_cores()
+    assert 1 <= hc["threads"] <= hc["affinity_cpus"] == len(os.sched_getaffinity(0))
+    assert "model" in hc

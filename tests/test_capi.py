@@ -61,16 +61,43 @@ def test_library_has_gfx950_code_object():
     assert b"gfx950" in blob
 
 
-def _gfx950_disassembly(lib_path, tmp_path):
-    llvm = "/opt/rocm/lib/llvm/bin"
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _gfx950_code_object(lib_path, tmp_path):
     fb, co = str(tmp_path / "fatbin"), str(tmp_path / "k.co")
     # -O binary with an explicit output file: objcopy never touches (rewrites) the library
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib_path, fb], check=True,
                    capture_output=True)
-    subprocess.run([llvm + "/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fb,
+    subprocess.run([LLVM + "/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fb,
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True, capture_output=True)
-    return subprocess.run([llvm + "/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+    return co
+
+
+def _gfx950_disassembly(lib_path, tmp_path):
+    co = _gfx950_code_object(lib_path, tmp_path)
+    return subprocess.run([LLVM + "/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
                           text=True).stdout
+
+
+def kernel_resources(lib_path, tmp_path):
+    """{kernel: {private_segment_fixed_size, vgpr_spill_count, sgpr_spill_count, vgpr_count}}
+    from the gfx950 code object's AMDHSA metadata note (llvm-readelf --notes)."""
+    co = _gfx950_code_object(lib_path, tmp_path)
+    notes = subprocess.run([LLVM + "/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                           text=True).stdout
+    res, cur = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s*-?\s*\.(\w+):\s+(\S+)", line)
+        if not m:
+            continue
+        key, val = m.groups()
+        if key == "name" and val.startswith("_Z"):
+            cur = res.setdefault(val, {})
+        elif cur is not None and key in ("private_segment_fixed_size", "vgpr_spill_count", "sgpr_spill_count",
+                                         "vgpr_count"):
+            cur[key] = int(val)
+    return res
 
 
 def test_kernels_use_no_flat_memory_ops(tmp_path):
@@ -85,6 +112,21 @@ def test_kernels_use_no_flat_memory_ops(tmp_path):
     assert re.search(r"\bds_read_b32\b", dis) and re.search(r"\bbuffer_load_dwordx4\b", dis)
     flat = [l.strip() for l in dis.splitlines() if re.search(r"\bflat_\w+", l)]
     assert not flat, flat[:5]
+
+
+@pytest.mark.parametrize("lib", ["libwtp_crc32.so", "libwtp_diag.so"])
+def test_kernels_use_no_scratch(lib, tmp_path):
+    """No kernel spills to scratch: every kernel's private segment is 0 bytes and its
+    spill counts are 0 (round 2's fused builder, at the generic 1024-thread launch bound,
+    spilled 192-240 VGPRs into 484 B of scratch per lane on every launch)."""
+    if not os.path.exists(LLVM + "/llvm-readelf"):
+        pytest.skip("no ROCm llvm tools")
+    res = kernel_resources(os.path.join(LIBDIR, lib), tmp_path)
+    assert len(res) >= (20 if lib == "libwtp_crc32.so" else 1), sorted(res)
+    bad = {k: v for k, v in res.items()
+           if v.get("private_segment_fixed_size", 0) or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0)}
+    assert not bad, bad
+    assert any("BuildBEpi" in k for k in res) or lib != "libwtp_crc32.so"
 
 
 def test_cpu_crc32_golden(golden):

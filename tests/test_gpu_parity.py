@@ -928,6 +928,27 @@ def test_host_chunked_pageable_and_pinned(W):
     pb.free()
 
 
+@pytest.mark.parametrize("parts", [2, 3, 4, 5, 6])
+def test_host_chunked_pageable_staging_split(W, parts):
+    """Pageable sources are staged into the pinned slab by up to 6 threads, one part each
+    (kMinPart = 8 MiB).  Sizes parts * 8 MiB + r (0 < r < parts) make floor(bytes / parts)
+    page-aligned while bytes % parts != 0: the last r bytes, i.e. the tail of the last
+    chunk, must still be copied (they were left stale)."""
+    for r in sorted({1, parts - 1}):
+        nbytes = parts * (8 << 20) + r
+        host = O.synth_fill_np(nbytes, start_byte=parts * 131 + r)
+        # run twice with different tails in between: stale slab bytes would show up
+        for rep in range(2):
+            host[-1] ^= np.uint8(0x5A * (rep + 1))
+            got = W.host_chunked(host, 1456)
+            n = got.size
+            assert got[-1] == O.crc32(host[(n - 1) * 1456:]), (parts, r, rep)
+            assert got[0] == O.crc32(host[:1456])
+        idx = np.arange(0, n - 1, 997)
+        want = [O.crc32(host[i * 1456:(i + 1) * 1456]) for i in idx]
+        assert np.array_equal(got[idx], np.array(want, np.uint32))
+
+
 def test_c3_1gib_host_chunked_elementwise(W):
     """Config C3 at full size: a 1 GiB host file (2^30 B -> 737,461 chunks, the last one
     64 B) through the pinned H2D -> CRC -> D2H pipeline, pageable and pinned sources,

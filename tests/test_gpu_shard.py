@@ -154,3 +154,20 @@ def test_bench_pipelined_gather_one_rank(W):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["config"]["gather"] and line["config"]["reserved_cus"] == 8
     assert line["parity"]["match"] is True, line["parity"]
+
+
+def test_bench_c4_shard_gather_one_rank(W):
+    """The per-rank work of the driver's `bench.py --gpus 8` (config C4: 2,097,152 x
+    1456 B per rank) through the pipelined RCCL gather in a one-rank world: the gathered
+    vector's sha256 equals the reference digest for 2 M packets (bench_digests.json)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gather-n1", "--packets-per-rank", "2097152",
+                        "--steps", "5", "--warmup", "5", "--no-cpu-baseline", "--no-probe"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["config"]["packets_per_rank"] == 2097152 and line["config"]["gather"]
+    assert line["parity"]["packets"] == 2097152 and line["parity"]["match"] is True, line["parity"]
