@@ -268,11 +268,13 @@ __device__ __forceinline__ void rotate_prio(uint32_t x) {
 // group ahead, the loads put() will need (so a flush never waits on memory).
 struct CrcBEpi {  // out[p] = crc
     static constexpr bool kCopy = false;  // see BuildBEpi
+    static constexpr bool kFixup = false;  // see VerifyBEpi
     static constexpr int kBound = 1024;   // __launch_bounds__ (launched at 512; kbench A/B builds at up to 1024)
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
     struct Pre {};
     __device__ __forceinline__ void pre(uint64_t, Pre &) const {}
+    __device__ __forceinline__ bool listed(bool, const Pre &) const { return false; }
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
         if (on) out[p] = v ^ cinit;
     }
@@ -281,17 +283,20 @@ struct CrcBEpi {  // out[p] = crc
 // ring's "full" payload length len (1456 for a WTP ring: 1472-B datagrams, whatever the
 // slot stride, e.g. wReceiver's 1504-B slots that hold a 1500-B recvfrom buffer).
 // Datagrams with recv_len == 16 + len are decided here (Receiver.cpp:203-206:
-// ntohl(header.checksum) == crc32(payload)); every other datagram goes to the fix-up
-// list, which the general kernel finishes.
+// ntohl(header.checksum) == crc32(payload)).  Every other datagram (short, empty, runt,
+// 1473-1500 B, oversize) first gets ok = 0, crc = 0, is counted, and the workgroup's
+// fix-up phase (verify_fixup, after its braided rounds) recomputes it with the
+// reference's semantics: one launch, no state outside the caller's buffers.
 struct VerifyBEpi {
     static constexpr bool kCopy = false;
+    static constexpr bool kFixup = true;  // see VerifyBEpi
     static constexpr int kBound = 1024;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
     uint64_t stride;
     uint8_t *ok;
     uint32_t *crc;  // may be null
-    uint32_t *fix;  // fix[0] = count, fix[1] = the fix-up pass's done counter, fix[2..] = indices
+    uint32_t *status;
     uint32_t cinit;
     uint64_t n;
     uint32_t full;  // recv_len of the datagrams this pass decides (16 + len)
@@ -304,15 +309,14 @@ struct VerifyBEpi {
         q.r = ((gu32 *)rl)[pc];
         q.h = *(gu32 *)((gu8 *)ring + pc * stride + 12);
     }
+    // true for a datagram the fix-up phase must finish
+    __device__ __forceinline__ bool listed(bool on, const Pre &q) const { return on && q.r != full; }
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &q) const {
         if (!on) return;
-        if (q.r == full) {
-            const uint32_t c = v ^ cinit;
-            ok[p] = bswap32(q.h) == c ? 1 : 0;
-            if (crc) crc[p] = c;
-        } else {
-            fix[2 + atomicAdd(fix, 1u)] = uint32_t(p);
-        }
+        const uint32_t c = v ^ cinit;
+        const bool mine = q.r == full;
+        ok[p] = mine && bswap32(q.h) == c ? 1 : 0;
+        if (crc) crc[p] = mine ? c : 0u;
     }
 };
 
@@ -325,6 +329,7 @@ struct VerifyBEpi {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes);
 struct BuildBEpi {
     static constexpr bool kCopy = true;
+    static constexpr bool kFixup = false;  // see VerifyBEpi
     // launched at 128 threads: the bound lets the copy rows keep their registers (at the
     // generic 1024 bound the compiler had 128 VGPRs and spilled 192-240 of them, 484 B of
     // scratch per lane)
@@ -348,6 +353,7 @@ struct BuildBEpi {
         // bytes, 1.2% faster; profiles/r01g/builder_store_ab.txt)
         __builtin_amdgcn_raw_buffer_store_b128(w, rs, int(o), 0, 0);
     }
+    __device__ __forceinline__ bool listed(bool, const Pre &) const { return false; }
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
         if (!on) return;
         const u32x4 h = {bswap32(WTP_TYPE_DATA), bswap32(seq0 + uint32_t(p)), bswap32(len), bswap32(v ^ cinit)};
@@ -355,6 +361,9 @@ struct BuildBEpi {
         if (wire_len) wire_len[p] = 16u + len;
     }
 };
+
+__device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, const uint32_t *gtab, uint32_t nfix,
+                                             uint64_t rstep, uint32_t wave, uint32_t lane);
 
 // k_fixed_braid<ROWS> — 16 lanes own one packet, a wave holds 4 packets per round.
 //
@@ -447,6 +456,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     uint32_t k = 0;            // rounds written to the slot since the last flush
     uint64_t rfirst = 0;       // round of slot row 0
     typename BEpi::Pre pre{};  // epilogue loads for the current group
+    uint32_t nfix = 0;         // datagrams this wave left to the fix-up phase (verify)
     auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rstep) * 4 + ((lane >> 1) & 3u); };
 
     auto flush = [&](uint64_t next_g0, bool more) {
@@ -478,7 +488,9 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // the advance T past the last row, deferred from the rounds (it commutes with
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
-        epi.put(p, acc, h == 0 && (lane >> 3) < k && rr < rounds && p < n, pre);
+        const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
+        epi.put(p, acc, on, pre);
+        if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
     };
@@ -577,6 +589,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     }
     if (k) flush(0, false);
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
+    if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------
@@ -804,70 +817,15 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 //      a packet's last piece emits crc = W ^ ~0.
 // Loads and stores are branch-free (out-of-range buffer offsets for idle lanes), so the
 // prefetches stay in flight across the round.
+// The piece-stream main loop: packets [lo, hi) of the provider (wpieces = their piece
+// total, for the work-left priority of variable-length providers), tables already in LDS
+// (PcTables).  Used by k_pieces and by the braided verify's fix-up phase.
 template <class Prov, class Epi>
-__global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
-                                                 uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
-                                                 uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
-    char *lds = reinterpret_cast<char *>(lds_w);
-    n = prov.count(n);  // device-side count for the fix-up pass
-    const uint32_t nw = blockDim.x >> 6;
-    const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
-    const uint64_t g0 = n * w0 / tw, g1 = n * (w0 + nw) / tw;  // this workgroup's packets
-    if (g0 == g1) {  // no packets for this block
-        if constexpr (Prov::kCounted) {
-            __syncthreads();  // every thread has read the count
-            if (threadIdx.x == 0) prov.done(gridDim.x);
-        }
-        return;
-    }
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
-    PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
-    WaveSplit split;
-    {
-        // every table load first (one memory latency, and ahead of the length loads of the
-        // wave split, since vmcnt completes in order; see StagFill): the staggered sets,
-        // the plain scan operators and the head-init table
-        constexpr uint32_t kOpQ = 5 * 256, kOpPer = (kOpQ + kPcThreads - 1) / kPcThreads;
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024);
-        const StagSet sets[2] = {{gtab + OFF_S4, 0u}, {gtab + OFF_FWD, 128u}};
-        StagFill<2, kPcThreads> fill;
-        fill.load(sets);
-        u32x4 q[kOpPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kOpPer; ++k) {
-            const uint32_t i = threadIdx.x + k * kPcThreads;
-            q[k] = src[i < kOpQ ? i : 0];
-        }
-        const uint32_t hv = gtab[OFF_HINIT + (threadIdx.x <= kPieceS ? threadIdx.x : 0)];
-        if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
-        PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
-        fill.store(lds, sets);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kPcOps);
-#pragma unroll
-        for (uint32_t k = 0; k < kOpPer; ++k) {
-            const uint32_t i = threadIdx.x + k * kPcThreads;
-            if (i < kOpQ) dst[i] = q[k];
-        }
-        if (threadIdx.x <= kPieceS) lds_w[kPcHinit / 4 + threadIdx.x] = hv;
-    }
-    uint64_t lo, hi;
-    uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
-    if constexpr (Prov::kVarLen) {
-        split.finish(prov, g0, g1, lds, wave, lane, lo, hi, wpieces);  // its barriers also publish the tables
-    } else {
-        lo = n * (w0 + wave) / tw;
-        hi = n * (w0 + wave + 1) / tw;
-        __syncthreads();
-    }
-    if constexpr (Prov::kCounted)
-        if (threadIdx.x == 0) prov.done(gridDim.x);  // after the barrier: the block has read the count
-    PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
-
+__device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs, const Prov &prov, const Epi &epi,
+                                            uint64_t lo, uint64_t hi, uint32_t wpieces, uint32_t *status,
+                                            uint32_t wave, uint32_t lane) {
     const StagKeys K(lane);
-    lchar *const slot = (lchar *)lds_w + kPcStage + wave * kPcSlot;
+    lchar *const slot = (lchar *)lds + kPcStage + wave * kPcSlot;
     constexpr int32_t kSpanBytes = int32_t(16 * kPcChunks);
     constexpr int32_t kNoSpan = 0x7FFFF000;  // out of range: loads return 0, no traffic
 
@@ -905,7 +863,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
 
         // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
         // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
-        lu8 *const flags = (lu8 *)lds_w + kPcFlags + wave * 64u;
+        lu8 *const flags = (lu8 *)lds + kPcFlags + wave * 64u;
         flags[lane] = 0;
         if (have && excl < 64u) flags[excl] = 1;
         __builtin_amdgcn_wave_barrier();
@@ -1035,8 +993,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
             done += total;
             const uint32_t left = wpieces > done ? wpieces - done : 0u;
             const uint32_t simd = wave & 3u;
-            if (lane == 0) lds_w[kPcRem / 4 + 4u * simd + (wave >> 2)] = left;
-            const u32x4 r4 = *(const lu32x4 *)((lchar *)lds_w + kPcRem + 16u * simd);
+            if (lane == 0) *(__attribute__((address_space(3))) uint32_t *)((lchar *)lds + kPcRem + 4u * (4u * simd + (wave >> 2))) = left;
+            const u32x4 r4 = *(const lu32x4 *)((lchar *)lds + kPcRem + 16u * simd);
             rotate_prio(uint32_t(r4.x < left) + uint32_t(r4.y < left) + uint32_t(r4.z < left) + uint32_t(r4.w < left));
         } else {
             rotate_prio(nrounds + (wave >> 2));
@@ -1045,6 +1003,204 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     PC_PROBE(6, nrounds);
     PC_PROBE(7, hi - lo);
+}
+
+// LDS tables of the piece loop: the two staggered sets (slice-by-4, x^(8*64)), the plain
+// scan operators x^(8*64*d), d = 2..32, and the head-init table.  load() issues every
+// global load (ahead of the caller's other prologue loads: vmcnt completes in order),
+// store() writes LDS; a barrier must follow before pieces_loop.
+template <int THREADS>
+struct PcTables {
+    static constexpr uint32_t kOpQ = 5 * 256, kOpPer = (kOpQ + THREADS - 1) / THREADS;
+    StagFill<2, THREADS> fill;
+    u32x4 q[kOpPer];
+    uint32_t hv;
+    __device__ __forceinline__ static void sets(const uint32_t *gtab, StagSet (&s)[2]) {
+        s[0] = {gtab + OFF_S4, 0u};
+        s[1] = {gtab + OFF_FWD, 128u};
+    }
+    __device__ __forceinline__ void load(const uint32_t *gtab) {
+        StagSet ss[2];
+        sets(gtab, ss);
+        fill.load(ss);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024);
+#pragma unroll
+        for (uint32_t k = 0; k < kOpPer; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            q[k] = src[i < kOpQ ? i : 0];
+        }
+        hv = gtab[OFF_HINIT + (threadIdx.x <= kPieceS ? threadIdx.x : 0)];
+    }
+    __device__ __forceinline__ void store(char *lds, const uint32_t *gtab) const {
+        StagSet ss[2];
+        sets(gtab, ss);
+        fill.store(lds, ss);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(lds + kPcOps);
+#pragma unroll
+        for (uint32_t k = 0; k < kOpPer; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            if (i < kOpQ) dst[i] = q[k];
+        }
+        if (threadIdx.x <= kPieceS) reinterpret_cast<uint32_t *>(lds + kPcHinit)[threadIdx.x] = hv;
+    }
+};
+
+template <class Prov, class Epi>
+__global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
+                                                 uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
+                                                 uint32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
+    char *lds = reinterpret_cast<char *>(lds_w);
+    const uint32_t nw = blockDim.x >> 6;
+    const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
+    const uint64_t g0 = n * w0 / tw, g1 = n * (w0 + nw) / tw;  // this workgroup's packets
+    if (g0 == g1) return;  // no packets for this block
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
+    PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
+    WaveSplit split;
+    {
+        // every table load first (one memory latency, and ahead of the length loads of the
+        // wave split, since vmcnt completes in order; see StagFill)
+        PcTables<kPcThreads> tb;
+        tb.load(gtab);
+        if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
+        PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
+        tb.store(lds, gtab);
+    }
+    uint64_t lo, hi;
+    uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
+    if constexpr (Prov::kVarLen) {
+        split.finish(prov, g0, g1, lds, wave, lane, lo, hi, wpieces);  // its barriers also publish the tables
+    } else {
+        lo = n * (w0 + wave) / tw;
+        hi = n * (w0 + wave + 1) / tw;
+        __syncthreads();
+    }
+    PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
+
+    pieces_loop(lds, rs, prov, epi, lo, hi, wpieces, status, wave, lane);
+}
+
+// ------------------------------------------------------------------------------------
+// 2a. verify fix-up phase (end of k_fixed_braid<VerifyBEpi>)
+// ------------------------------------------------------------------------------------
+// The braided verify decides the datagrams of the ring's full length; every other one
+// (short, empty, runt, 1473-1500 B in a 1504-B slot, oversize) was given ok = 0, crc = 0
+// and counted by its wave's flush (nfix).  Once all waves of the workgroup are past their
+// braided rounds, a workgroup that counted none returns (one barrier: the common case
+// costs nothing).  Otherwise it rebuilds its LDS for the piece loop (PcTables), rescans
+// its own packets in passes of kVfPass, compacts the listed ones into an LDS index list
+// and finishes them with pieces_loop (DgramProvL semantics: CRC over [16, recv_len),
+// Receiver.cpp:25-35,203-206).  Nothing lives outside the caller's buffers and the
+// kernel: no list in global memory, no counters, no second launch, so any number of
+// concurrent calls, streams and graph replays are independent.  A rescan that finds a
+// different number of datagrams than the flushes counted (the recv_len array changed
+// under the kernel) sets status bit 2.
+//
+// LDS after the braided rounds (the piece layout for 8 waves): tables [0, kPcStage),
+// staging slots of waves 0..7, the index list where slots 8..15 of k_pieces would be,
+// flags at kPcFlags, control words (per-wave counts, list length) past kPcLdsWords.
+constexpr uint32_t kVfWaves = 8;  // the verify launch's 512 threads (kBraidThreads)
+constexpr uint32_t kVfList = kPcStage + kVfWaves * kPcSlot;
+constexpr uint32_t kVfCap = (kPcFlags - kVfList) / 4;
+constexpr uint32_t kVfCtl = (kPcLdsWords * 4 + 15) & ~15u;
+constexpr uint32_t kVfPer = 8;                          // packets rescanned per thread and pass
+constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
+static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fix-up LDS");
+
+typedef __attribute__((address_space(3))) uint32_t lu32;
+
+// Datagram list[p] of the ring (lead 0: the ring is 16-B aligned); aux = ntohl(checksum).
+struct LdsIdxDgramProv {
+    static constexpr bool kVarLen = false;
+    static constexpr bool kIndexed = true;
+    uint64_t stride;
+    const uint32_t *__restrict__ rl;
+    const lu32 *list;
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
+        const uint32_t idx = list[p];
+        const uint32_t h = uint32_t(uint64_t(idx) * stride + 12);  // 4-B aligned, the view is < 2 GiB
+        r.a = idx;
+        r.b = rl[idx];
+        const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(h), 0, 0));
+        r.c = w.x;
+        r.d = w.y;
+    }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
+                                           uint32_t &slot) const {
+        const uint64_t d = r.a * stride;
+        want = bswap32(r.c);  // d + 12 is 4-B aligned
+        off = d + 16;
+        ok = r.b >= 16 && r.b <= stride;
+        l = ok ? r.b - 16 : 0;
+        slot = uint32_t(r.a);
+    }
+};
+
+__device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, const uint32_t *gtab, uint32_t nfix,
+                                             uint64_t rstep, uint32_t wave, uint32_t lane) {
+    lu32 *const ctl = (lu32 *)((lchar *)lds + kVfCtl);  // [w] = wave w's count, [8] = list length
+    const uint32_t nwave = blockDim.x >> 6;
+    if (lane == 0) ctl[wave] = nfix;
+    __syncthreads();  // every wave is past its braided rounds and flushes
+    uint32_t total = 0;
+    for (uint32_t w = 0; w < nwave; ++w) total += ctl[w];
+    total = __builtin_amdgcn_readfirstlane(total);
+    if (total == 0) return;
+    typedef __attribute__((address_space(1))) uint32_t gmu32;
+    gmu32 *const st = (gmu32 *)epi.status;
+    if (nwave != kVfWaves) {  // the host launches 512 threads; anything else cannot hold the list
+        if (threadIdx.x == 0) __hip_atomic_fetch_or(st, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    {
+        PcTables<kVfWaves * 64> tb;  // overwrites the braid tables: no wave reads them any more
+        tb.load(gtab);
+        tb.store(lds, gtab);
+    }
+    const uint64_t n = epi.n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(epi.ring, uint32_t((n * epi.stride + 15) & ~uint64_t(15)));
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(epi.rl, uint32_t(4 * n));
+    lu32 *const list = (lu32 *)((lchar *)lds + kVfList);
+    const LdsIdxDgramProv prov{epi.stride, epi.rl, list};
+    const VerifyEpi vepi{epi.ok, epi.crc, uint32_t(n)};
+    const uint64_t g0 = uint64_t(blockIdx.x) * nwave;  // the workgroup's first round
+    uint32_t found = 0;
+    // the workgroup's packets in braided order: enumeration index e <-> packet
+    // 4 (g0 + (e >> 5) rstep) + (e & 31) (wave (e & 31) >> 2's round of group e >> 5)
+    for (uint64_t e0 = 0; 4 * (g0 + (e0 >> 5) * rstep) < n; e0 += kVfPass) {
+        if (threadIdx.x == 0) ctl[8] = 0;
+        __syncthreads();  // publishes the tables (first pass) and the reset list length
+        uint64_t pv[kVfPer];
+        uint32_t rv[kVfPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kVfPer; ++k) {
+            const uint64_t e = e0 + k * (kVfWaves * 64) + threadIdx.x;
+            pv[k] = 4 * (g0 + (e >> 5) * rstep) + (e & 31u);
+            rv[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, pv[k] < n ? int(4 * pv[k]) : int(0x80000000u), 0, 0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kVfPer; ++k) {
+            const bool need = pv[k] < n && rv[k] != epi.full;
+            const uint64_t m = __ballot(need);
+            if (m == 0) continue;  // wave-uniform
+            uint32_t b = 0;
+            if (lane == 0) b = __hip_atomic_fetch_add(&ctl[8], uint32_t(__popcll(m)), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            b = __builtin_amdgcn_readfirstlane(b);
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            if (need) list[b + pos] = uint32_t(pv[k]);
+        }
+        __syncthreads();
+        const uint32_t c = __builtin_amdgcn_readfirstlane(ctl[8]);
+        found += c;
+        const uint64_t lo = uint64_t(c) * wave / kVfWaves, hi = uint64_t(c) * (wave + 1) / kVfWaves;
+        pieces_loop(lds, rs, prov, vepi, lo, hi, 0u, epi.status, wave, lane);
+        __syncthreads();  // the next pass rebuilds the list
+    }
+    if (threadIdx.x == 0 && found != total) __hip_atomic_fetch_or(st, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1482,18 +1638,9 @@ struct DevState {
     int cus = 0;
     std::atomic<int> reserve{0};  // CUs left free of the persistent kernels (wtp_reserve_cus)
     unsigned grid_cus() const { return unsigned(std::max(1, cus - reserve.load(std::memory_order_relaxed))); }
-    hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed
-    // verify fix-up lists, one per stream (kernels of one stream never overlap): zeroed
-    // once when allocated, then reset by the fix-up pass itself (IdxDgramProvL)
-    struct FixSlot {
-        uint32_t *buf = nullptr;
-        uint64_t cap = 0;  // u32 entries
-    };
-    std::mutex fix_mu;
-    std::unordered_map<hipStream_t, FixSlot> fix_slots;
+    hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed (builder scratch)
 };
 constexpr int kMaxDev = 64;
-constexpr size_t kMaxFixSlots = 256;  // verify fix-up slots per device (one per stream used)
 DevState g_dev[kMaxDev];
 
 std::vector<uint32_t> host_tables() {
@@ -1542,7 +1689,7 @@ int init_device(int dev) {
                 return setfail(WTP_EHIP, "hipMemcpy(tables) failed");
             if (hipMalloc(&s.status, 4) != hipSuccess) return setfail(WTP_ENOMEM, "hipMalloc(status) failed");
             if (hipMemset(s.status, 0, 4) != hipSuccess) return setfail(WTP_EHIP, "hipMemset(status) failed");
-            // Scratch of async entry points (verify fix-up list, builder CRCs) comes from a
+            // Scratch of async entry points (the builder's CRCs on its slow path) comes from a
             // library-owned pool whose memory is kept across calls (release threshold max):
             // the default threshold returns it at every synchronisation, and re-mapping it
             // cost ~1 ms per small host-verify call.
@@ -1670,12 +1817,10 @@ namespace dev {
 // raw words into (offset in the view, length, valid, aux, output slot) when the round
 // uses them.  count(n) is the number of packets (device-side for the fix-up pass).
 struct FixedProvL {
-    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     uint32_t len;
-    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
                                            uint32_t &) const {
@@ -1685,13 +1830,11 @@ struct FixedProvL {
     }
 };
 struct ArrayProvL {
-    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
-    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
         r.a = reinterpret_cast<const uint32_t *>(offs)[2 * p];  // low dword: the view is < 2 GiB
         r.b = lens[p];
@@ -1712,12 +1855,10 @@ struct ArrayProvL {
 // the last datagram, reads there return 0 and are never selected) and are
 // funnel-shifted at decode.
 struct DgramProvL {
-    static constexpr bool kCounted = false;  // see IdxDgramProvL
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
-    __device__ __forceinline__ uint64_t count(uint64_t n) const { return n; }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
         const uint32_t h = uint32_t(lead + p * stride + 12) & ~3u;  // the view is < 2 GiB
         r.a = p;
@@ -1736,51 +1877,6 @@ struct DgramProvL {
         off = d + 16;
         ok = r.b >= 16 && r.b <= stride;
         l = ok ? r.b - 16 : 0;
-    }
-};
-// The fix-up pass of the braided verify: datagrams fix[1 .. fix[0]] of the ring (in
-// whatever order the atomics left them).  The index load makes this provider's other
-// loads dependent (it only sees the rare short or malformed datagrams).
-// The list lives in a per-(device, stream) slot that outlives the call: fix[0] = count,
-// fix[1] = workgroups done, fix[2 ..] = indices.  Every workgroup of this pass reads the
-// count, then adds itself to fix[1]; the last one zeroes both, so the slot is ready for
-// the next call on the stream with no memset or allocation per call.
-struct IdxDgramProvL {
-    static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
-    static constexpr bool kIndexed = true;
-    static constexpr bool kCounted = true;
-    uint64_t stride, lead;
-    const uint32_t *__restrict__ rl;
-    uint32_t *fix;
-    uint32_t nidx;  // datagrams of the batch (>= 1): listed indices are clamped below it
-    __device__ __forceinline__ uint64_t count(uint64_t n) const {
-        const uint64_t c = *(const __attribute__((address_space(1))) uint32_t *)fix;  // written by the braid pass
-        return c < n ? c : n;
-    }
-    __device__ __forceinline__ void done(uint32_t grid) const {
-        if (atomicAdd(fix + 1, 1u) == grid - 1) {
-            __atomic_store_n(fix, 0u, __ATOMIC_RELAXED);
-            __atomic_store_n(fix + 1, 0u, __ATOMIC_RELAXED);
-        }
-    }
-    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
-        const uint32_t i0 = fix[2 + p];
-        const uint32_t idx = i0 < nidx ? i0 : nidx - 1;  // a listed index is < nidx unless the slot was shared
-        const uint32_t h = uint32_t(lead + uint64_t(idx) * stride + 12) & ~3u;
-        r.a = idx;
-        r.b = rl[idx];
-        const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(h), 0, 0));
-        r.c = w.x;
-        r.d = w.y;
-    }
-    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &want,
-                                           uint32_t &slot) const {
-        const uint64_t d = lead + r.a * stride;
-        want = bswap32(__builtin_amdgcn_alignbyte(r.d, r.c, uint32_t(d + 12) & 3u));
-        off = d + 16;
-        ok = r.b >= 16 && r.b <= stride;
-        l = ok ? r.b - 16 : 0;
-        slot = uint32_t(r.a);
     }
 };
 }  // namespace dev
@@ -1921,76 +2017,25 @@ int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t *b = static_cast<const uint8_t *>(d_dgrams);
-    // Braided fast path for a 16-B aligned ring: it decides every datagram of the ring's
-    // full WTP length 16 + min(stride - 16, 1456) (1472 B in wReceiver's 1504-B slots or
-    // in a packed 1472-B ring); the rest (short, empty, 1473-1500 B, malformed) are
-    // listed on the device and the general kernel finishes them, reading its packet
-    // count from the list.
+    // Braided fast path for a 16-B aligned ring: one launch per sub-batch decides every
+    // datagram of the ring's full WTP length 16 + min(stride - 16, 1456) (1472 B in
+    // wReceiver's 1504-B slots or in a packed 1472-B ring); each workgroup then finishes
+    // the rest of its own datagrams (short, empty, 1473-1500 B, malformed) in its fix-up
+    // phase (verify_fixup).  No memory outside the caller's buffers, so captures, graph
+    // replays and concurrent calls on any streams need nothing from the host.  The
+    // sub-batches keep each launch's ring view below 2 GiB (32-bit buffer offsets).
     if (stride % 16 == 0 && stride >= 32 && stride <= 16384 && reinterpret_cast<uintptr_t>(b) % 16 == 0) {
         const uint32_t flen = uint32_t(std::min<size_t>(stride - 16, WTP_MAX_PAYLOAD));
-        const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);  // fix-up view < 2 GiB
-        const uint64_t need = 2 + std::min<uint64_t>(per, n);
-        // The fix-up list is the stream's persistent slot: zeroed once when allocated,
-        // then reset by the fix-up pass itself.  No allocation ever happens inside a graph
-        // capture: a capture uses the capturing stream's slot if an earlier call on that
-        // stream made one large enough (the graph then shares it with the stream: replay
-        // it on that stream, or not concurrently with the stream's other verify calls);
-        // otherwise the call takes the general kernel below, which needs no list.  So does
-        // hipStreamPerThread (one handle, a different stream in every host thread).  Slots
-        // are keyed by handle: a stream destroyed with a verify still in flight whose
-        // handle a new stream then reuses would share its slot with that verify (the
-        // fix-up pass clamps every listed index to the batch, so a shared slot can give
-        // wrong results but never an out-of-bounds access).
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        WTP_HIP(hipStreamIsCapturing(st, &cs));
-        const bool capturing = cs != hipStreamCaptureStatusNone;
-        std::unique_lock<std::mutex> lk(s->fix_mu, std::defer_lock);  // held until the launches are queued
-        uint32_t *fix = nullptr;
-        if (st != hipStreamPerThread) {
-            lk.lock();
-            if (capturing) {
-                auto it = s->fix_slots.find(st);
-                if (it != s->fix_slots.end() && it->second.cap >= need) fix = it->second.buf;
-            } else {
-                if (s->fix_slots.size() >= kMaxFixSlots && !s->fix_slots.count(st)) {
-                    // bounded: a process that cycles through many streams (destroyed ones
-                    // keep their entries) drops every slot once the device is idle
-                    WTP_HIP(hipDeviceSynchronize());
-                    for (auto &kv : s->fix_slots) (void)hipFreeAsync(kv.second.buf, nullptr);  // device idle
-                    s->fix_slots.clear();
-                }
-                DevState::FixSlot &slot = s->fix_slots[st];
-                if (slot.cap < need) {
-                    if (slot.buf) WTP_HIP(hipFreeAsync(slot.buf, st));  // after the stream's earlier uses
-                    slot.buf = nullptr;
-                    slot.cap = 0;
-                    uint32_t *nb = nullptr;
-                    WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&nb), 4 * need, s->pool, st));
-                    if (hipMemsetAsync(nb, 0, 8, st) != hipSuccess) {
-                        (void)hipFreeAsync(nb, st);
-                        return fail(WTP_EHIP, "hipMemsetAsync failed");
-                    }
-                    slot.buf = nb;
-                    slot.cap = need;
-                }
-                fix = slot.buf;
-            }
+        const uint64_t per = std::min<uint64_t>(kSubBatch, ((1ull << 31) - 4096) / stride);
+        for (uint64_t p = 0; p < n && !rc; p += per) {
+            const uint64_t cnt = std::min<uint64_t>(per, n - p);
+            const uint8_t *sb = b + p * stride;
+            rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
+                                    dev::VerifyBEpi{d_recv_len + p, sb, stride, d_ok + p,
+                                                    d_crc_out ? d_crc_out + p : nullptr, s->status, 0, cnt, 16u + flen},
+                                    st);
         }
-        if (fix) {
-            for (uint64_t p = 0; p < n && !rc; p += per) {
-                const uint64_t cnt = std::min<uint64_t>(per, n - p);
-                const uint8_t *sb = b + p * stride;
-                uint8_t *ok = d_ok + p;
-                uint32_t *crc = d_crc_out ? d_crc_out + p : nullptr;
-                rc = launch_fixed_braid(*s, sb + 16, stride, flen, cnt,
-                                        dev::VerifyBEpi{d_recv_len + p, sb, stride, ok, crc, fix, 0, cnt, 16u + flen}, st);
-                if (!rc)
-                    rc = launch_pieces(*s, sb, cnt * stride, dev::IdxDgramProvL{stride, 0, d_recv_len + p, fix, uint32_t(cnt)}, cnt,
-                                       dev::VerifyEpi{ok, crc, uint32_t(cnt)}, st);
-            }
-            if (rc) (void)hipMemsetAsync(fix, 0, 8, st);  // a braid pass whose fix-up pass never ran left a count
-            return rc;
-        }
+        return rc;
     }
     const uint64_t per = std::min<uint64_t>(kSubBatch, std::max<uint64_t>(1, (1ull << 30) / stride));
     for (uint64_t p = 0; p < n; p += per) {

@@ -565,7 +565,7 @@ def _verify_dev(W, buf, stride, rl, n, with_crc=True, offset=0):
 
 
 @pytest.mark.parametrize("n,stride,frac,with_crc", [
-    (3001, 1472, 0.9, True),    # braided fast path + fix-up list
+    (3001, 1472, 0.9, True),    # braided fast path + in-kernel fix-up phase
     (3001, 1472, 0.9, False),   # no crc output
     (517, 1472, 1.0, True),     # every datagram full
     (400, 1488, 0.0, True),     # 16-B stride, no datagram full: all through the fix-up
@@ -622,12 +622,12 @@ def test_verify_wreceiver_1504_slots(W, n):
     assert np.array_equal(ok2, want_ok) and np.array_equal(crc2, want_crc)
 
 
-def test_verify_fixup_slot_reuse(W):
-    """The fix-up list is a per-stream slot the fix-up pass resets itself: back-to-back
-    calls on one stream (growing and shrinking batches), calls on a second stream, an
-    all-full ring (empty list) between them, hipStreamPerThread from two threads (general
-    kernel), and CUDA-graph captures on a fresh stream (general kernel) and on a stream
-    with a slot (the slot), each replayed twice, all stay bit-exact."""
+def test_verify_calls_are_independent(W):
+    """The braided verify keeps no state between calls (each workgroup finishes its own
+    short/odd datagrams in its fix-up phase): back-to-back calls on one stream (growing
+    and shrinking batches), calls on a second stream, an all-full ring (no fix-up work)
+    between them, hipStreamPerThread from two threads, and CUDA-graph captures on a fresh
+    stream and on a stream that verified before, each replayed twice, all bit-exact."""
     rng = np.random.default_rng(2024)
     stride = 1504
     rings = {}
@@ -667,8 +667,8 @@ def test_verify_fixup_slot_reuse(W):
         for n in (3001, 64):
             outs.append((n, *run(n)))
     torch.cuda.synchronize()
-    # hipStreamPerThread (handle 2): a different stream in every host thread, so it takes
-    # the general kernel (no list); two threads at once
+    # hipStreamPerThread (handle 2): a different stream in every host thread; two threads
+    # at once
     import threading
     res = {}
 
@@ -687,8 +687,8 @@ def test_verify_fixup_slot_reuse(W):
             assert bool(ok.all())
         else:
             check(n, ok, crc)
-    # graph capture never allocates: on a fresh stream the captured call takes the
-    # general kernel (no list); on a stream with a slot it uses that slot
+    # graph capture: the captured call is one kernel node whose only memory is the
+    # caller's buffers
     d, r, _, _ = rings[3001]
     for warm in (False, True):
         gok = torch.full((3001,), 7, dtype=torch.uint8, device="cuda")
@@ -710,12 +710,13 @@ def test_verify_fixup_slot_reuse(W):
                 g.replay()
             torch.cuda.synchronize()
             check(3001, gok, gcrc)
-            check(97, *run(97))  # the default stream's slot is untouched by the graph
+            check(97, *run(97))  # calls on the default stream between replays
 
 
-def test_verify_many_streams_slot_bound(W):
-    """More streams than the library keeps fix-up slots for (256 per device): the slots
-    are dropped and rebuilt; every call on every stream stays bit-exact."""
+def test_verify_many_streams(W):
+    """300 streams, one verify each, all in flight together (round 2 kept a fix-up slot
+    per stream and had to drop them past 256; now nothing is kept): every call on every
+    stream is bit-exact."""
     import ctypes as C
     hip = C.CDLL("libamdhip64.so")
     rng = np.random.default_rng(77)
@@ -745,10 +746,10 @@ def test_verify_many_streams_slot_bound(W):
             hip.hipStreamDestroy(h)
 
 
-def test_verify_sub_batches_share_the_slot(W):
+def test_verify_sub_batches(W):
     """A ring longer than one fast-path launch takes (stride 16384: 131,071 datagrams per
-    sub-batch, the fix-up view < 2 GiB): two sub-batches reuse one fix-up slot, each
-    with short and corrupt datagrams of its own, including both sides of the boundary."""
+    sub-batch, each launch's ring view < 2 GiB): two launches, each with short and
+    corrupt datagrams of its own, including both sides of the boundary."""
     stride, n = 16384, 140_000
     per = ((1 << 31) - 4096) // stride
     assert n > per
@@ -784,6 +785,82 @@ def test_verify_sub_batches_share_the_slot(W):
     intact[short] = False
     intact[flip] = False
     assert got_ok[intact].all()
+
+
+def test_verify_graph_replay_after_larger_call_on_its_stream(W):
+    """a graph captured on a stream, then a larger verify on that stream (round
+    2 then freed the stream's fix-up slot that the graph had baked in), then the graph
+    replayed: bit-exact, and so is the larger call."""
+    rng = np.random.default_rng(55)
+    stride = 1504
+    small, big = 3001, 20000
+    rings = {}
+    for n in (small, big):
+        buf, rl = _wtp_ring(n, stride, rng)
+        want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+        rings[n] = (dev_u8(buf), torch.from_numpy(rl.view(np.int32)).cuda(), want_ok, want_crc)
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    d, r, want_ok, want_crc = rings[small]
+    gok = torch.full((small,), 7, dtype=torch.uint8, device="cuda")
+    gcrc = u32_out(small)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(cs):
+        W.verify_batch(d, stride, r, small, gok, gcrc, stream=cs)
+        cs.synchronize()
+        g.capture_begin()
+        W.verify_batch(d, stride, r, small, gok, gcrc)
+        g.capture_end()
+        d2, r2, want_ok2, want_crc2 = rings[big]
+        ok2 = torch.full((big,), 7, dtype=torch.uint8, device="cuda")
+        crc2 = u32_out(big)
+        W.verify_batch(d2, stride, r2, big, ok2, crc2)
+        for _ in range(2):
+            gok.fill_(7)
+            gcrc.fill_(-1)
+            g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(gok.cpu().numpy(), want_ok) and np.array_equal(to_u32(gcrc, small), want_crc)
+    assert np.array_equal(ok2.cpu().numpy(), want_ok2) and np.array_equal(to_u32(crc2, big), want_crc2)
+
+
+@pytest.mark.parametrize("stride,frac_full", [(1472, 0.0), (1504, 0.3)])
+def test_verify_fixup_multi_pass(W, stride, frac_full):
+    """More fix-up datagrams per workgroup than one rescan pass covers (4096 packets):
+    with all but 6 CUs reserved, 6 workgroups own 30,000 datagrams (~5,000 each), so
+    every workgroup's fix-up phase runs two passes; every ok/crc is written (prefilled
+    with 7 / 0xFFFFFFFF) and equals the oracle."""
+    rng = np.random.default_rng(stride)
+    n = 30000
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    rl = np.zeros(n, dtype=np.uint32)
+    body = O.synth_fill_np(n * 1456, start_byte=17)
+    for i in range(n):
+        L = 1456 if rng.random() < frac_full else int(rng.integers(0, min(stride - 16, 1484) + 1))
+        if L == 1456 and stride > 1472 and rng.random() < 0.5:
+            L = int(rng.integers(1457, stride - 15))
+        dg = O.build_datagram(i, body[i * 1456:i * 1456 + min(L, 1456)].tobytes() + bytes(max(0, L - 1456)))
+        buf[i * stride:i * stride + len(dg)] = np.frombuffer(dg, dtype=np.uint8)
+        rl[i] = len(dg)
+    bad = rng.choice(n, 300, replace=False)
+    for i in bad:
+        if rl[i] > 16:
+            buf[i * stride + 16 + int(rng.integers(0, rl[i] - 16))] ^= 0x08
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    W.reserve_cus(cus - 6, 0)
+    try:
+        d = dev_u8(buf)
+        r = torch.from_numpy(rl.view(np.int32)).cuda()
+        ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        crc = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        W.verify_batch(d, stride, r, n, ok, crc)
+        torch.cuda.synchronize()
+    finally:
+        W.reserve_cus(0, 0)
+    assert np.array_equal(ok.cpu().numpy(), want_ok), np.nonzero(ok.cpu().numpy() != want_ok)[0][:10]
+    assert np.array_equal(to_u32(crc, n), want_crc)
+    assert W.device_status(0, clear=True) == 0
 
 
 def test_verify_misaligned_ring_takes_general_path(W):

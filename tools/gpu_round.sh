@@ -36,6 +36,8 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;        # the driver's invocation
     bench2) run bench2 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench200) run bench200 400 python bench.py --no-cpu-baseline ;;
+    c4shard) run c4shard 400 python bench.py --steps 20 --warmup 5 --packets-per-rank 2097152 --no-cpu-baseline ;;
+    c4gather) run c4gather 400 python bench.py --steps 20 --warmup 5 --gather-n1 --packets-per-rank 2097152 --no-cpu-baseline ;;
     prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
            cd "$ROOT" ;;
