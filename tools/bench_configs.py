@@ -28,24 +28,37 @@ import torch  # noqa: E402
 import oracle as O  # noqa: E402
 import wtp_crc32 as W  # noqa: E402
 
+sys.path.insert(0, ROOT)
+from bench import TimingEvent  # noqa: E402
+
 GB = 1e9
 GIB = float(1 << 30)
 PEAK = 8000.0
 
 
 def timed(fn, reps, warm=3):
+    """(median per-call ms with an event between calls, mean ms per call back to back).
+    Events are timing-only (hipEventDisableSystemFence, bench.TimingEvent): a default
+    event's system-scope cache flush pads every interval and slows the next launch.  The
+    back-to-back figure has no event between the calls at all: one pair around `reps`."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
-    ev[0].record()
+    st = torch.cuda.current_stream()
+    ev = [TimingEvent() for _ in range(reps + 1)]
+    ev[0].record(st)
     for i in range(reps):
         fn()
-        ev[i + 1].record()
+        ev[i + 1].record(st)
     torch.cuda.synchronize()
     ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))
-    tot = ev[0].elapsed_time(ev[reps])
-    return ts[len(ts) // 2], tot / reps
+    a, b = TimingEvent(), TimingEvent()
+    a.record(st)
+    for _ in range(reps):
+        fn()
+    b.record(st)
+    torch.cuda.synchronize()
+    return ts[len(ts) // 2], a.elapsed_time(b) / reps
 
 
 def graph_time(fn, G=50, reps=7, per=10):
@@ -217,25 +230,111 @@ def verify():
     gv2, _ = graph_time(f2)
     good2 = int(ok.sum().item())
     del w2, rl2
+    # the same 1472-B ring with three short datagrams (START/END-like 16-B ones and a
+    # short last chunk): their workgroups run the in-kernel fix-up phase
     wl = torch.empty(n, dtype=torch.int32, device="cuda")
+    W.build_data_packets(payload, n * 1456, 0, wire, stride, wl)
+    wl3 = wl.clone()
+    wl3[0], wl3[n // 2], wl3[n - 1] = 16, 16, 1016
+    f3 = lambda: W.verify_batch(wire, stride, wl3, n, ok)  # noqa: E731
+    med3, mean3 = timed(f3, 100)
+    gv3, _ = graph_time(f3)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy()
+    want3 = okh.sum() == n - 3 and okh[0] == 0 and okh[n - 1] == 0  # short datagrams fail their checksum
+    del wl3
     return [{"config": "receiver verify, 1M x 1472-B datagrams device-resident", "packets": n,
-             "ms_per_launch": round(mean, 4), "payload_GiBps": round(n * 1456 / (mean * 1e-3) / GIB, 1),
+             "ms_per_launch": round(mean, 4), "per_call_ms_median_with_events": round(med, 4),
+             "payload_GiBps": round(n * 1456 / (mean * 1e-3) / GIB, 1),
              "read_GBps": round(n * (stride + 4) / (mean * 1e-3) / GB, 1), "graph_ms_per_launch": round(gv, 4),
              "graph_frac_hbm": round(n * (stride + 4) / (gv * 1e-3) / GB / PEAK, 4), "all_ok": good == n},
             {"config": "receiver verify, 1M x 1472-B datagrams in 1504-B slots (wReceiver ring)", "packets": n,
-             "ms_per_launch": round(mean2, 4), "payload_GiBps": round(n * 1456 / (mean2 * 1e-3) / GIB, 1),
+             "ms_per_launch": round(mean2, 4), "per_call_ms_median_with_events": round(med2, 4),
+             "payload_GiBps": round(n * 1456 / (mean2 * 1e-3) / GIB, 1),
              "read_GBps": round(n * (stride + 4) / (mean2 * 1e-3) / GB, 1), "graph_ms_per_launch": round(gv2, 4),
              "graph_frac_hbm": round(n * (stride + 4) / (gv2 * 1e-3) / GB / PEAK, 4), "all_ok": good2 == n},
+            {"config": "receiver verify, 1M x 1472-B ring with 3 short datagrams (in-kernel fix-up)", "packets": n,
+             "ms_per_launch": round(mean3, 4), "per_call_ms_median_with_events": round(med3, 4),
+             "graph_ms_per_launch": round(gv3, 4), "graph_frac_hbm": round(n * (stride + 4) / (gv3 * 1e-3) / GB / PEAK, 4),
+             "ok_pattern_as_expected": bool(want3)},
             {"config": "fused DATA packet builder, 1M x 1456 B -> 1472-B wire slots", "packets": n,
              "ms_per_launch": round(bmean, 4), "GBps_read_plus_write": round(n * (1456 + 1472) / (bmean * 1e-3) / GB, 1),
              "d2d_copy_same_bytes_GBps_read_plus_write": round(2 * n * 1456 / (cmean * 1e-3) / GB, 1),
              "first_datagram_matches_oracle": h[:1472] == want}]
 
 
+def hostverify():
+    """Receiver side end to end (north_star: the path ends in host memory): wReceiver's
+    ring of 1504-B slots in pinned memory (wtp_host_alloc, as its recvmmsg ring) with a
+    pinned recv_len array -> wtp_crc32_host_verify (H2D of the ring + lengths, the braided
+    verify, D2H of ok + crc) at window-size batches and a 1 GiB ring; and the same from a
+    pageable numpy ring (staged through the library's pinned slabs).  All datagrams are
+    full 1472-B WTP DATA datagrams except the last of each batch (short)."""
+    stride = 1504
+    out = {"config": "receiver end to end: host ring of 1504-B slots -> wtp_crc32_host_verify -> host ok/crc",
+           "stride": stride, "rows": []}
+    nmax = (1 << 30) // stride
+    ring = W.PinnedBuffer(nmax * stride)
+    lens = W.PinnedBuffer(nmax * 4)
+    la = lens.array.view(np.uint32)
+    # build nmax datagrams on the device, copy into the pinned ring
+    payload = torch.empty(nmax * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(payload, start_byte=7)
+    wire = torch.zeros(nmax * stride, dtype=torch.uint8, device="cuda")
+    wl = torch.empty(nmax, dtype=torch.int32, device="cuda")
+    W.build_data_packets(payload, nmax * 1456, 0, wire, stride, wl)
+    ring.array[:] = wire.cpu().numpy()
+    la[:] = wl.cpu().numpy().view(np.uint32)
+    del payload, wire, wl
+    torch.cuda.empty_cache()
+    okb = np.zeros(nmax, np.uint8)
+    crcb = np.zeros(nmax, np.uint32)
+    import ctypes as C
+
+    def call(buf_ptr, lens_ptr, n):
+        rc = W.LIB.wtp_crc32_host_verify(buf_ptr, stride, lens_ptr, n, okb.ctypes.data, crcb.ctypes.data)
+        assert rc == 0, W.LIB.wtp_last_error()
+
+    pageable = np.empty(nmax * stride, np.uint8)
+    pageable[:] = ring.array
+    plens = la.copy()
+    for n in (10, 64, 1024, 16384, nmax):
+        for kind, bp, lp in (("pinned", ring.ptr, lens.ptr), ("pageable", pageable.ctypes.data, plens.ctypes.data)):
+            # last datagram of the batch short: the fix-up phase runs, as with a file's tail
+            save_p, save_l = la[n - 1], plens[n - 1]
+            la[n - 1] = plens[n - 1] = 16 + 100
+            reps = 5 if n == nmax else (200 if n <= 1024 else 50)
+            call(bp, lp, n)
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                call(bp, lp, n)
+                ts.append(time.perf_counter() - t0)
+            t = float(np.median(ts))
+            good = int(okb[:n].sum())
+            la[n - 1], plens[n - 1] = save_p, save_l
+            by = n * stride
+            out["rows"].append({"n": n, "source": kind, "ring_bytes": by, "median_ms": round(t * 1e3, 4),
+                                "ring_GBps": round(by / t / GB, 2), "payload_GiBps": round(n * 1456 / t / GIB, 2),
+                                "datagrams_per_s": round(n / t), "ok_all_but_last": good == n - 1 and okb[n - 1] == 0})
+            print(json.dumps(out["rows"][-1]), flush=True)
+    # the link itself: pinned H2D of the 1 GiB ring
+    d = torch.empty(nmax * stride, dtype=torch.uint8, device="cuda")
+    ht = torch.from_numpy(ring.array)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d.copy_(ht, non_blocking=True)
+    torch.cuda.synchronize()
+    out["raw_h2d_pinned_GBps"] = round(nmax * stride / (time.perf_counter() - t0) / GB, 2)
+    ring.free()
+    lens.free()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="configs.json")
-    ap.add_argument("--only", default="c2,c3,c5,verify")
+    ap.add_argument("--only", default="c2,c3,c5,verify,hostverify")
     a = ap.parse_args()
     assert W.LIB.wtp_init(0) == 0
     res = {"device": torch.cuda.get_device_name(0), "host_cpus": os.cpu_count(), "results": []}
@@ -250,6 +349,8 @@ def main():
         res["results"].extend(verify())
     if "c3" in sel:
         res["results"].append(c3())
+    if "hostverify" in sel:
+        res["results"].append(hostverify())
     for r in res["results"]:
         print(json.dumps(r), flush=True)
     with open(a.out, "w") as f:
