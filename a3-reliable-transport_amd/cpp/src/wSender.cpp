@@ -13,10 +13,14 @@
 // (wtp_crc32_host_chunked_multi over N devices with --gpus N, 0 = all), or with the
 // reference's per-packet crc32() with --crc cpu.  Retransmissions reuse the stored header.
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 #include <iterator>
 #include <random>
+#include <vector>
 
 #include "common/Endpoint.hpp"
 
@@ -31,12 +35,27 @@ class InputFile {
     InputFile(const std::string &path, bool pinned) : pinned_(pinned) {
         std::FILE *f = std::fopen(path.c_str(), "rb");
         if (!f) throw std::runtime_error("cannot open " + path);
-        std::fseek(f, 0, SEEK_END);
-        const long sz = std::ftell(f);
-        std::fseek(f, 0, SEEK_SET);
-        n_ = sz > 0 ? size_t(sz) : 0;
-        p_ = static_cast<uint8_t *>(pinned ? wtp_host_alloc(n_) : std::malloc(n_ ? n_ : 1));
-        const bool ok = p_ && std::fread(p_, 1, n_, f) == n_;
+        long sz = -1;
+        if (std::fseek(f, 0, SEEK_END) == 0) {
+            sz = std::ftell(f);
+            if (std::fseek(f, 0, SEEK_SET) != 0) sz = -1;
+        }
+        bool ok;
+        if (sz >= 0) {  // a regular file: one read into a buffer of its size
+            n_ = size_t(sz);
+            p_ = alloc(n_);
+            ok = p_ && std::fread(p_, 1, n_, f) == n_;
+        } else {  // a pipe, /dev/stdin, process substitution: read until EOF
+            std::vector<uint8_t> v;
+            uint8_t buf[1 << 16];
+            size_t got;
+            while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) v.insert(v.end(), buf, buf + got);
+            ok = !std::ferror(f);
+            n_ = v.size();
+            p_ = alloc(n_);
+            ok = ok && p_;
+            if (ok && n_) std::memcpy(p_, v.data(), n_);
+        }
         std::fclose(f);
         if (!ok) {
             release();
@@ -50,6 +69,9 @@ class InputFile {
     size_t size() const { return n_; }
 
    private:
+    uint8_t *alloc(size_t n) const {
+        return static_cast<uint8_t *>(pinned_ ? wtp_host_alloc(n) : std::malloc(n ? n : 1));
+    }
     void release() {
         if (pinned_)
             wtp_host_free(p_);

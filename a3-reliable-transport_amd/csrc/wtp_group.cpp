@@ -14,6 +14,7 @@ extern "C" int wtp_set_error_(int code, const char *msg);
 struct wtp_group {
     std::vector<int> dev;
     std::vector<ncclComm_t> comm;
+    bool aborted = false;  // a gather failed inside its RCCL group: communicators aborted
 };
 
 namespace {
@@ -67,7 +68,8 @@ int wtp_group_create(const int *devices, int ndev, wtp_group **out) {
 
 void wtp_group_destroy(wtp_group *g) {
     if (!g) return;
-    for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
+    if (!g->aborted)
+        for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
     delete g;
 }
 
@@ -77,8 +79,11 @@ int wtp_group_crc32_fixed_gather(wtp_group *g, const void *const *d_shards, size
                                  const size_t *n_per, uint32_t *const *d_local, uint32_t *d_out, int root,
                                  void *const *streams) {
     if (!g || !d_shards || !n_per || !d_local || !d_out) return gfail(WTP_EINVAL, "null pointer");
+    if (g->aborted) return gfail(WTP_EHIP, "group aborted by an earlier failed gather; destroy and recreate it");
     const int R = int(g->dev.size());
     if (root < 0 || root >= R) return gfail(WTP_EINVAL, "root out of range");
+    for (int r = 0; r < R; ++r)
+        if (!d_local[r] || (n_per[r] && !d_shards[r])) return gfail(WTP_EINVAL, "null shard or result pointer");
     auto st = [&](int r) { return streams ? static_cast<hipStream_t>(streams[r]) : hipStream_t(nullptr); };
     // 1. every rank checksums its shard (the braided kernel for 1456-B payloads)
     for (int r = 0; r < R; ++r) {
@@ -87,11 +92,20 @@ int wtp_group_crc32_fixed_gather(wtp_group *g, const void *const *d_shards, size
         });
         if (rc) return rc;
     }
-    // 2. gather to the root, stream-ordered after each rank's kernel
+    // 2. gather to the root, stream-ordered after each rank's kernel.  Every device is
+    // made current once before the group opens, so nothing expected can fail between
+    // ncclGroupStart and ncclGroupEnd; if an enqueue still fails there, the ops already
+    // posted for other ranks would wait for peers that never post theirs, so the
+    // communicators are aborted (and the group refuses further use) instead.
     bool equal = true;
     for (int r = 1; r < R; ++r) equal = equal && n_per[r] == n_per[0];
     int prev = 0;
     (void)hipGetDevice(&prev);
+    for (int r = 0; r < R; ++r)
+        if (hipSetDevice(g->dev[r]) != hipSuccess) {
+            (void)hipSetDevice(prev);
+            return gfail(WTP_ENODEV, "hipSetDevice(" + std::to_string(g->dev[r]) + ") failed");
+        }
     ncclResult_t res = ncclGroupStart();
     if (res != ncclSuccess) return nccl_fail("ncclGroupStart", res);
     int rc = WTP_OK;
@@ -121,6 +135,12 @@ int wtp_group_crc32_fixed_gather(wtp_group *g, const void *const *d_shards, size
     }
     res = ncclGroupEnd();
     if (rc == WTP_OK && res != ncclSuccess) rc = nccl_fail("ncclGroupEnd", res);
+    if (rc != WTP_OK) {
+        for (ncclComm_t c : g->comm) (void)ncclCommAbort(c);
+        g->aborted = true;
+        (void)hipSetDevice(prev);
+        return rc;
+    }
     // the root's own shard (ragged path): a device-local copy behind its kernel
     if (rc == WTP_OK && !equal && n_per[root] && hipSetDevice(g->dev[root]) == hipSuccess) {
         if (hipMemcpyAsync(d_out + off_root, d_local[root], n_per[root] * 4, hipMemcpyDeviceToDevice, st(root)) !=

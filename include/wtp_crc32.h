@@ -130,14 +130,12 @@ int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t
    (0 for runts and malformed lengths).  Fast path: a 16-B aligned ring with
    stride % 16 == 0 (e.g. 1472 = header + 1456, or wReceiver's 1504-B slots holding the
    reference's 1500-B receive buffer) runs the braided kernel over the first
-   min(stride - 16, 1456) payload bytes of every slot, decides the datagrams of exactly
-   that length, and finishes the others in a second, general-kernel pass.  That pass
-   reads a list of the others which the library keeps per (device, stream) for the
-   life of the process: no allocation or memset per call.  Captured into a graph, a call
-   uses the capturing stream's list if an earlier call on that stream created one (the
-   graph then shares it with that stream: replay it on that stream, or not concurrently
-   with the stream's other verify calls); otherwise, and on hipStreamPerThread, the
-   call runs the general kernel alone (no list, nothing allocated). */
+   min(stride - 16, 1456) payload bytes of every slot and decides the datagrams of
+   exactly that length; in the same launch each workgroup then finishes its other
+   datagrams (short, empty, 1473-1500 B, malformed) with the general algorithm.  The
+   call uses no memory besides the caller's buffers and keeps no state between calls:
+   graph captures, replays on any stream and concurrent calls are independent.  Status
+   bit 2 (wtp_device_status): the recv_len array changed while the kernel ran. */
 int wtp_crc32_verify_batch(const void *d_dgrams, size_t stride, const uint32_t *d_recv_len,
                            size_t n, uint8_t *d_ok, uint32_t *d_crc_out, void *stream);
 

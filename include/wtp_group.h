@@ -37,7 +37,10 @@ int wtp_group_size(const wtp_group *g);
    Their CRCs go to d_local[r] (n_per[r] u32 on that device), then to d_out on the root
    rank's device in rank order (sum of n_per entries).  Equal shard sizes use one
    ncclGather; ragged ones grouped ncclSend/ncclRecv.  streams[r] is a hipStream_t of
-   rank r's device (streams == NULL or a NULL entry: the null stream). */
+   rank r's device (streams == NULL or a NULL entry: the null stream).  Every device is
+   made current before the RCCL group opens; if an enqueue nevertheless fails inside the
+   group, the communicators are aborted (no rank waits for a peer that never posted) and
+   every later call on g fails: destroy it and create a new one. */
 int wtp_group_crc32_fixed_gather(wtp_group *g, const void *const *d_shards, size_t stride, size_t len,
                                  const size_t *n_per, uint32_t *const *d_local, uint32_t *d_out, int root,
                                  void *const *streams);

@@ -148,6 +148,29 @@ def test_c1_corruption_loss_reorder(binaries, tmp_path):
             assert ck == want[seq]
 
 
+def test_c1_nonseekable_input(binaries, golden, tmp_path):
+    """wSender -i on a FIFO (ftell fails on a pipe): the whole stream is read and sent,
+    byte-identical, with the golden chunk CRCs (a pipe used to send an empty
+    file)."""
+    import threading
+    src = os.path.join(GOLD, "input.txt")
+    data = open(src, "rb").read()
+    fifo = str(tmp_path / "in.fifo")
+    os.mkfifo(fifo)
+
+    def feed():
+        with open(fifo, "wb") as f:
+            for i in range(0, len(data), 1000):  # in pieces, as a pipe delivers them
+                f.write(data[i:i + 1000])
+
+    t = threading.Thread(target=feed, daemon=True)
+    t.start()
+    out, slog, rlog, _ = run_transfer(binaries, fifo, str(tmp_path))
+    t.join(timeout=10)
+    assert open(out, "rb").read() == data
+    assert [f"0x{c:08X}" for c in data_log_checksums(slog)] == golden["files"]["input.txt"]["crc"]
+
+
 @pytest.mark.gpu
 def test_c1_loopback_gpu_crc(binaries, golden, tmp_path):
     torch = pytest.importorskip("torch")
