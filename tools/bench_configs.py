@@ -316,7 +316,7 @@ def hostverify():
             by = n * stride
             out["rows"].append({"n": n, "source": kind, "ring_bytes": by, "median_ms": round(t * 1e3, 4),
                                 "ring_GBps": round(by / t / GB, 2), "payload_GiBps": round(n * 1456 / t / GIB, 2),
-                                "datagrams_per_s": round(n / t), "ok_all_but_last": good == n - 1 and okb[n - 1] == 0})
+                                "datagrams_per_s": round(n / t), "ok_all_but_last": bool(good == n - 1 and okb[n - 1] == 0)})
             print(json.dumps(out["rows"][-1]), flush=True)
     # the link itself: pinned H2D of the 1 GiB ring
     d = torch.empty(nmax * stride, dtype=torch.uint8, device="cuda")
@@ -339,22 +339,24 @@ def main():
     assert W.LIB.wtp_init(0) == 0
     res = {"device": torch.cuda.get_device_name(0), "host_cpus": os.cpu_count(), "results": []}
     sel = a.only.split(",")
+    def add(*rs):
+        for r in rs:
+            res["results"].append(r)
+            print(json.dumps(r), flush=True)
+            with open(a.out, "w") as f:  # after every result: a later failure keeps the earlier ones
+                json.dump(res, f, indent=1)
+
     if "c2" in sel:
-        res["results"].append(c2())
+        add(c2())
     if "c5" in sel:
         for entry in ("stream", "var", "packed"):
-            res["results"].append(c5(1.1, entry))
-            res["results"].append(c5(1.0, entry))
+            add(c5(1.1, entry), c5(1.0, entry))
     if "verify" in sel:
-        res["results"].extend(verify())
+        add(*verify())
     if "c3" in sel:
-        res["results"].append(c3())
+        add(c3())
     if "hostverify" in sel:
-        res["results"].append(hostverify())
-    for r in res["results"]:
-        print(json.dumps(r), flush=True)
-    with open(a.out, "w") as f:
-        json.dump(res, f, indent=1)
+        add(hostverify())
 
 
 if __name__ == "__main__":

@@ -65,6 +65,7 @@ for s in $STEPS; do
              v=$(basename "$lib" .so)
              WTP_LIB="$ROOT/$lib" run "ab_$v" 300 python tools/bench_configs.py --only "${CFG_ONLY:-c5}" --out "$OUT/ab_$v.json"
            done ;;
+    split) run split 300 python tools/split_probe.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done
