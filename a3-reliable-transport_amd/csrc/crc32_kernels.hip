@@ -269,7 +269,8 @@ __device__ __forceinline__ void rotate_prio(uint32_t x) {
 struct CrcBEpi {  // out[p] = crc
     static constexpr bool kCopy = false;  // see BuildBEpi
     static constexpr bool kFixup = false;  // see VerifyBEpi
-    static constexpr int kBound = 1024;   // __launch_bounds__ (launched at 512; kbench A/B builds at up to 1024)
+    static constexpr int kThreads = 512;  // the launcher's workgroup size (launch_fixed_braid)
+    static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
     struct Pre {};
@@ -290,6 +291,7 @@ struct CrcBEpi {  // out[p] = crc
 struct VerifyBEpi {
     static constexpr bool kCopy = false;
     static constexpr bool kFixup = true;  // see VerifyBEpi
+    static constexpr int kThreads = 512;  // verify_fixup's LDS layout assumes 8 waves
     static constexpr int kBound = 1024;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
@@ -327,13 +329,17 @@ struct VerifyBEpi {
 // per row, out-of-range offset for chunks outside the packet), so the payload is read
 // from HBM once; the header follows at the flush.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t nbytes);
+#ifndef WTP_BUILD_THREADS
+#define WTP_BUILD_THREADS 128  // fused builder workgroup size (A/B builds: 256, 512)
+#endif
 struct BuildBEpi {
     static constexpr bool kCopy = true;
     static constexpr bool kFixup = false;  // see VerifyBEpi
     // launched at 128 threads: the bound lets the copy rows keep their registers (at the
     // generic 1024 bound the compiler had 128 VGPRs and spilled 192-240 of them, 484 B of
     // scratch per lane)
-    static constexpr int kBound = 128;
+    static constexpr int kThreads = WTP_BUILD_THREADS;
+    static constexpr int kBound = WTP_BUILD_THREADS;
     uint8_t *wire;
     uint64_t wstride;  // multiple of 16
     uint32_t seq0, len;
@@ -546,7 +552,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
                              {gtab + OFF_INV + 0 * 1024, 128u},
                              {gtab + OFF_INV + 2 * 1024, 65536u},
                              {gtab + OFF_INV + 5 * 1024, 65536u + 128u}};
-    constexpr int kT = BEpi::kCopy ? 128 : 512;  // the launcher's workgroup sizes
+    constexpr int kT = BEpi::kThreads;  // the launcher's workgroup size
     StagFill<4, kT> fill;
     const bool batched = blockDim.x == kT;  // other sizes: tools/kbench.hip A/B builds
 #ifndef WTP_BR_PROLOGUE_DIAG  // probe builds only: 1 = no table loads, 2 = no table fill at all
@@ -1734,8 +1740,8 @@ int launch_check(const char *what) {
 // Fewer waves per CU keep fewer rows in flight; HBM serves the stream with less
 // queueing (and, for the builder, fewer read/write turnarounds) while 8 resp. 2 waves,
 // two rounds each, still cover its latency.
-constexpr unsigned kBraidThreads = 512;
-constexpr unsigned kBuildThreads = 128;
+constexpr unsigned kBraidThreads = dev::CrcBEpi::kThreads;
+static_assert(dev::VerifyBEpi::kThreads == dev::CrcBEpi::kThreads, "one braided grid rule");
 
 template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
@@ -1750,7 +1756,7 @@ template <class BEpi>
 int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
                        hipStream_t st) {
     const int rows = int((len + 255) / 256);
-    const unsigned threads = BEpi::kCopy ? kBuildThreads : kBraidThreads;
+    const unsigned threads = BEpi::kThreads;
     const uint64_t rounds = (n + 3) / 4;
     const uint64_t want = (rounds + threads / 64 - 1) / (threads / 64);
     uint64_t cap = s.grid_cus();

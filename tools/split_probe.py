@@ -31,7 +31,8 @@ def step(parts):
 
 
 variants = {"2M x1": lambda: step(1), "1M x2": lambda: step(2), "512K x4": lambda: step(4), "256K x8": lambda: step(8),
-            "1M alone": lambda: W.crc32_batch_fixed(buf, P, P, n // 2, out)}
+            "1M alone": lambda: W.crc32_batch_fixed(buf, P, P, n // 2, out),
+            "1M second half": lambda: W.crc32_batch_fixed(buf[(n // 2) * P:], P, P, n // 2, out)}
 for _ in range(150):
     step(1)
 torch.cuda.synchronize()
@@ -47,7 +48,7 @@ for rep in range(12):
         res[k].append(a.elapsed_time(b) / 10 * 1e3)
 summary = {}
 for k, v in res.items():
-    byts = (n // 2 if k == "1M alone" else n) * P
+    byts = (n // 2 if k.startswith("1M ") else n) * P
     med = float(np.median(v))
     summary[k] = {"median_us": round(med, 1), "mean_us": round(float(np.mean(v)), 1), "TBps": round(byts / med / 1e6, 3)}
 print(json.dumps(summary, indent=1))
