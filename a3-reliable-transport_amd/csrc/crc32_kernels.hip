@@ -270,6 +270,7 @@ struct CrcBEpi {  // out[p] = crc
     static constexpr bool kCopy = false;  // see BuildBEpi
     static constexpr bool kFixup = false;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // the launcher's workgroup size (launch_fixed_braid)
+    static constexpr int kDepth = 2;      // register sets in the main loop (rounds in flight + 1)
     static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
@@ -292,6 +293,7 @@ struct VerifyBEpi {
     static constexpr bool kCopy = false;
     static constexpr bool kFixup = true;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // verify_fixup's LDS layout assumes 8 waves
+    static constexpr int kDepth = 2;
     static constexpr int kBound = 1024;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
@@ -332,6 +334,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 #ifndef WTP_BUILD_THREADS
 #define WTP_BUILD_THREADS 128  // fused builder workgroup size (A/B builds: 256, 512)
 #endif
+#ifndef WTP_BUILD_DEPTH
+#define WTP_BUILD_DEPTH 2  // fused builder register sets (A/B builds: 3)
+#endif
 struct BuildBEpi {
     static constexpr bool kCopy = true;
     static constexpr bool kFixup = false;  // see VerifyBEpi
@@ -339,6 +344,7 @@ struct BuildBEpi {
     // generic 1024 bound the compiler had 128 VGPRs and spilled 192-240 of them, 484 B of
     // scratch per lane)
     static constexpr int kThreads = WTP_BUILD_THREADS;
+    static constexpr int kDepth = WTP_BUILD_DEPTH;
     static constexpr int kBound = WTP_BUILD_THREADS;
     uint8_t *wire;
     uint64_t wstride;  // multiple of 16
@@ -582,16 +588,37 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // waves per CU +0.9% sustained (kbench x4, profiles/r01i/kbench_512_prio.log; it lost
     // 1% at 16 waves).  DIAG bit2 turns it off for ablations.
     uint32_t prio_round = wave >> 2;
-    while (r < rounds) {
-        if (!(DIAG & 4)) rotate_prio(++prio_round);
+    if constexpr (BEpi::kDepth == 3) {
+        // three register sets, two rounds in flight while one is hashed (the fused
+        // builder: only 2 waves per CU, so each wave keeps more bytes in flight)
+        Round C;
         load_round(r + rstep, B);
-        crc_round(r, A);
-        if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
-        r += rstep;
-        if (r >= rounds) break;
-        load_round(r + rstep, A);
-        crc_round(r, B);
-        r += rstep;
+        while (r < rounds) {
+            if (!(DIAG & 4)) rotate_prio(++prio_round);
+            load_round(r + 2 * rstep, C);
+            crc_round(r, A);
+            r += rstep;
+            if (r >= rounds) break;
+            load_round(r + 2 * rstep, A);
+            crc_round(r, B);
+            r += rstep;
+            if (r >= rounds) break;
+            load_round(r + 2 * rstep, B);
+            crc_round(r, C);
+            r += rstep;
+        }
+    } else {
+        while (r < rounds) {
+            if (!(DIAG & 4)) rotate_prio(++prio_round);
+            load_round(r + rstep, B);
+            crc_round(r, A);
+            if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
+            r += rstep;
+            if (r >= rounds) break;
+            load_round(r + rstep, A);
+            crc_round(r, B);
+            r += rstep;
+        }
     }
     if (k) flush(0, false);
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
