@@ -271,6 +271,7 @@ struct CrcBEpi {  // out[p] = crc
     static constexpr bool kFixup = false;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // the launcher's workgroup size (launch_fixed_braid)
     static constexpr int kDepth = 2;      // register sets in the main loop (rounds in flight + 1)
+    static constexpr int kDiag = 0;       // DIAG of the production instantiation
     static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     uint32_t *out;
     uint32_t cinit;  // init_const(len)
@@ -294,6 +295,7 @@ struct VerifyBEpi {
     static constexpr bool kFixup = true;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // verify_fixup's LDS layout assumes 8 waves
     static constexpr int kDepth = 2;
+    static constexpr int kDiag = 0;
     static constexpr int kBound = 1024;
     const uint32_t *rl;
     const uint8_t *ring;  // 16-B aligned, stride % 16 == 0: header words are aligned
@@ -334,6 +336,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 #ifndef WTP_BUILD_THREADS
 #define WTP_BUILD_THREADS 128  // fused builder workgroup size (A/B builds: 256, 512)
 #endif
+#ifndef WTP_BUILD_DIAG
+#define WTP_BUILD_DIAG 0
+#endif
 #ifndef WTP_BUILD_DEPTH
 #define WTP_BUILD_DEPTH 2  // fused builder register sets (A/B builds: 3)
 #endif
@@ -345,6 +350,7 @@ struct BuildBEpi {
     // scratch per lane)
     static constexpr int kThreads = WTP_BUILD_THREADS;
     static constexpr int kDepth = WTP_BUILD_DEPTH;
+    static constexpr int kDiag = WTP_BUILD_DIAG;  // ablation builds only (wrong CRCs)
     static constexpr int kBound = WTP_BUILD_THREADS;
     uint8_t *wire;
     uint64_t wstride;  // multiple of 16
@@ -850,25 +856,30 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 //      a packet's last piece emits crc = W ^ ~0.
 // Loads and stores are branch-free (out-of-range buffer offsets for idle lanes), so the
 // prefetches stay in flight across the round.
+// Metadata of packets q0 .. q0+63 for one round: lane i loads packet q0 + i (clamped to
+// hi - 1: branch-free).  The caller of pieces_loop issues the first round's (raw) before
+// its last prologue waits, so that latency overlaps them.
+template <class Prov>
+__device__ __forceinline__ void pieces_meta(const Prov &prov, uint64_t q0, uint64_t hi, uint32_t lane, MetaRaw &raw,
+                                            __amdgpu_buffer_rsrc_t rs) {
+    const uint64_t pi = q0 + lane;
+    prov.load(pi < hi ? pi : hi - 1, raw, rs);
+}
+
 // The piece-stream main loop: packets [lo, hi) of the provider (wpieces = their piece
 // total, for the work-left priority of variable-length providers), tables already in LDS
-// (PcTables).  Used by k_pieces and by the braided verify's fix-up phase.
+// (PcTables), raw = the first round's metadata (pieces_meta(lo)).  Used by k_pieces and
+// by the braided verify's fix-up phase.
 template <class Prov, class Epi>
 __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs, const Prov &prov, const Epi &epi,
                                             uint64_t lo, uint64_t hi, uint32_t wpieces, uint32_t *status,
-                                            uint32_t wave, uint32_t lane) {
+                                            uint32_t wave, uint32_t lane, MetaRaw raw) {
     const StagKeys K(lane);
     lchar *const slot = (lchar *)lds + kPcStage + wave * kPcSlot;
     constexpr int32_t kSpanBytes = int32_t(16 * kPcChunks);
     constexpr int32_t kNoSpan = 0x7FFFF000;  // out of range: loads return 0, no traffic
 
-    // lane i describes packet q0 + i (clamped to hi - 1: branch-free)
-    MetaRaw raw{};
-    auto meta = [&](uint64_t q0) {
-        const uint64_t pi = q0 + lane;
-        prov.load(pi < hi ? pi : hi - 1, raw, rs);
-    };
-    if (lo < hi) meta(lo);
+    auto meta = [&](uint64_t q0) { pieces_meta(prov, q0, hi, lane, raw, rs); };
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loop entry then matches its back edge
 
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
@@ -1093,27 +1104,29 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
     PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
     WaveSplit split;
-    {
-        // every table load first (one memory latency, and ahead of the length loads of the
-        // wave split, since vmcnt completes in order; see StagFill)
-        PcTables<kPcThreads> tb;
-        tb.load(gtab);
-        if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
-        PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
-        tb.store(lds, gtab);
-    }
+    PcTables<kPcThreads> tb;
+    // every table load first (one memory latency, and ahead of the length loads of the
+    // wave split, since vmcnt completes in order; see StagFill).  (Lengths first, tables
+    // behind them, the first round's metadata issued before the table stores wait:
+    // neutral on C5, 53.4 vs 52.9 us back to back, profiles/r03f/abc5.log.)
+    tb.load(gtab);
+    if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
+    PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
+    tb.store(lds, gtab);
     uint64_t lo, hi;
     uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
     if constexpr (Prov::kVarLen) {
-        split.finish(prov, g0, g1, lds, wave, lane, lo, hi, wpieces);  // its barriers also publish the tables
+        split.finish(prov, g0, g1, lds, wave, lane, lo, hi, wpieces);  // two barriers; LDS outside the tables
     } else {
         lo = n * (w0 + wave) / tw;
         hi = n * (w0 + wave + 1) / tw;
-        __syncthreads();
     }
+    MetaRaw raw{};
+    if (lo < hi) pieces_meta(prov, lo, hi, lane, raw, rs);
+    __syncthreads();  // the tables are visible to every wave
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
 
-    pieces_loop(lds, rs, prov, epi, lo, hi, wpieces, status, wave, lane);
+    pieces_loop(lds, rs, prov, epi, lo, hi, wpieces, status, wave, lane, raw);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1230,7 +1243,9 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
         const uint32_t c = __builtin_amdgcn_readfirstlane(ctl[8]);
         found += c;
         const uint64_t lo = uint64_t(c) * wave / kVfWaves, hi = uint64_t(c) * (wave + 1) / kVfWaves;
-        pieces_loop(lds, rs, prov, vepi, lo, hi, 0u, epi.status, wave, lane);
+        MetaRaw raw{};
+        if (lo < hi) pieces_meta(prov, lo, hi, lane, raw, rs);
+        pieces_loop(lds, rs, prov, vepi, lo, hi, 0u, epi.status, wave, lane, raw);
         __syncthreads();  // the next pass rebuilds the list
     }
     if (threadIdx.x == 0 && found != total) __hip_atomic_fetch_or(st, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1773,7 +1788,7 @@ static_assert(dev::VerifyBEpi::kThreads == dev::CrcBEpi::kThreads, "one braided 
 template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
                        uint64_t n, BEpi epi, const uint32_t *tabs) {
-    hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, 0, BEpi>), grid, dim3(threads), 0, st, b,
+    hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, BEpi::kDiag, BEpi>), grid, dim3(threads), 0, st, b,
                        uint32_t(stride), len, n, epi, tabs);
 }
 

@@ -67,6 +67,7 @@ for s in $STEPS; do
            done ;;
     split) run split 300 python tools/split_probe.py ;;
     footprint) run footprint 300 python tools/footprint_probe.py ;;
+    copyprobe) run copyprobe 120 ./tools/bin/copyprobe ;;
     abbuild) run abbuild 300 python tools/ab_lib.py --what build ${AB_LIBS} ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
