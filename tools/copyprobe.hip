@@ -5,6 +5,9 @@
 //   slot   : payload -> slot + 16, 16 B per lane, write-back stores
 //   slotnt : the same with nt loads and nt stores
 //   slotu4 : slot copy, 4 x 16 B per lane in flight (more bytes per wave before the waits)
+//   wslot  : iterate over wire chunks instead: 64-B aligned full-segment stores, loads
+//            16-B aligned only (the wire payload sits 16 B into a 64-B aligned slot)
+//   wslotnt: the same with nt loads and nt stores
 // Prints read+write GB/s per variant (HIP events, 50 launches after 20 warmups).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -24,6 +27,20 @@ __global__ __launch_bounds__(256) void k_slot(const uint8_t *__restrict__ s, uin
         const uint64_t p = i / c, k = i - p * c;
         const u32x4 *src = reinterpret_cast<const u32x4 *>(s + i * 16);
         u32x4 *dst = reinterpret_cast<u32x4 *>(d + p * kW + 16 + k * 16);
+        if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src), dst);
+        else *dst = *src;
+    }
+}
+
+// wire chunk m of slot p (m = 1..91 payload, m = 0 header: skipped) <- payload chunk m - 1
+template <int NT>
+__global__ __launch_bounds__(256) void k_wslot(const uint8_t *__restrict__ s, uint8_t *__restrict__ d, uint64_t nw16) {
+    constexpr uint64_t c = kW / 16;  // 92 chunks per slot
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < nw16; i += uint64_t(gridDim.x) * 256) {
+        const uint64_t p = i / c, k = i - p * c;
+        if (k == 0) continue;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(s + p * kL + (k - 1) * 16);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(d + i * 16);
         if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src), dst);
         else *dst = *src;
     }
@@ -82,6 +99,10 @@ int main() {
         printf("{\"variant\": \"slot\", \"grid\": %u, \"ms\": %.4f, \"GBps_rw\": %.1f}\n", g, t, rw / t / 1e6);
         t = time_ms([&] { hipLaunchKernelGGL(k_slot<1>, dim3(g), dim3(256), 0, 0, s, d, n16); });
         printf("{\"variant\": \"slotnt\", \"grid\": %u, \"ms\": %.4f, \"GBps_rw\": %.1f}\n", g, t, rw / t / 1e6);
+        t = time_ms([&] { hipLaunchKernelGGL(k_wslot<0>, dim3(g), dim3(256), 0, 0, s, d, kN * kW / 16); });
+        printf("{\"variant\": \"wslot\", \"grid\": %u, \"ms\": %.4f, \"GBps_rw\": %.1f}\n", g, t, rw / t / 1e6);
+        t = time_ms([&] { hipLaunchKernelGGL(k_wslot<1>, dim3(g), dim3(256), 0, 0, s, d, kN * kW / 16); });
+        printf("{\"variant\": \"wslotnt\", \"grid\": %u, \"ms\": %.4f, \"GBps_rw\": %.1f}\n", g, t, rw / t / 1e6);
         t = time_ms([&] { hipLaunchKernelGGL(k_slot4, dim3(g), dim3(256), 0, 0, s, d, n16); });
         printf("{\"variant\": \"slotu4\", \"grid\": %u, \"ms\": %.4f, \"GBps_rw\": %.1f}\n", g, t, rw / t / 1e6);
     }

@@ -32,6 +32,7 @@ nproc > "$OUT/host_cpus.txt"; lscpu 2>/dev/null | grep -m1 "Model name" >> "$OUT
 
 for s in $STEPS; do
   case "$s" in
+    testsvar) run gpu_tests_var 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -rf --timeout=300 --timeout-method thread -k "var or packed or zipf or mixed or every_length or smoke" ;;
     tests) run gpu_tests 900 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;        # the driver's invocation
     bench2) run bench2 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
@@ -68,7 +69,9 @@ for s in $STEPS; do
     split) run split 300 python tools/split_probe.py ;;
     footprint) run footprint 300 python tools/footprint_probe.py ;;
     copyprobe) run copyprobe 120 ./tools/bin/copyprobe ;;
+    ualprobe) run ualprobe 120 ./tools/bin/ualprobe ;;
     abbuild) run abbuild 300 python tools/ab_lib.py --what build ${AB_LIBS} ;;
+    abc5env) run abc5env 300 python tools/ab_c5_env.py --out "$OUT/abc5env.json" ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
