@@ -53,6 +53,7 @@ constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
 constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
 constexpr int kPieceS = 64;                  // piece bytes in the general kernel
 constexpr uint32_t kMaxVarLen = 4096;
+constexpr uint32_t kPsMaxLen = 64, kPsMinOff = 64;  // k_pieces' small packets (ps_small)
 constexpr uint64_t kSubBatch = 1ull << 28;      // packets per general-kernel launch (32-bit store offsets)        // 64 pieces x 64 B: one packet per wave max
 
 constexpr uint32_t OFF_BRAID = 0;            // 4x256 braid word tables (advance 256 B)
@@ -90,6 +91,7 @@ typedef __attribute__((address_space(3))) char lchar;
 typedef __attribute__((address_space(3))) u32x4 lu32x4;
 typedef __attribute__((address_space(3))) u32x2 lu32x2;
 typedef __attribute__((address_space(3))) uint8_t lu8;
+typedef __attribute__((address_space(3))) uint32_t lu32;
 
 // Per-wave phase timestamps for tools/pprobe.hip (built with -DWTP_PROBE=1 there and
 // compiled out of the product): slot k of wave (block, wave) gets value v, e.g. a
@@ -757,9 +759,15 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 __device__ __forceinline__ uint32_t pieces_of_len(uint32_t len) {
     return (len == 0 || len > kMaxVarLen) ? 1u : (len + kPieceS - 1) / kPieceS;
 }
+// pieces a packet takes in the piece stream (the wave split's estimate: small packets,
+// done by the small-packet phase, count 0 whatever their offset)
+template <class Prov>
+__device__ __forceinline__ uint32_t split_pieces(uint32_t len) {
+    return (Prov::kSmall && len <= kPsMaxLen) ? 0u : pieces_of_len(len);
+}
 template <class Prov>
 __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
-    return pieces_of_len(prov.len_of(prov.load_len(p)));
+    return split_pieces<Prov>(prov.len_of(prov.load_len(p)));
 }
 
 // Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
@@ -782,6 +790,30 @@ constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThrea
 #ifndef WTP_PC_LAG
 #define WTP_PC_LAG 1  // k_pieces: wave priority by work left (0: rotate by round and age)
 #endif
+#ifndef WTP_PC_SMALL
+#define WTP_PC_SMALL 0  // k_pieces, offset/length arrays: small-packet phase (measured slower; 1: A/B builds)
+#endif
+#ifndef WTP_PS_DIAG
+#define WTP_PS_DIAG 0  // ablation builds only (wrong CRCs): 1 no small rounds, 2 no small phase at all (the piece loop still skips)
+#endif
+// Small packets (k_pieces' small-packet phase): 0 <= len <= 64 and starting at view offset
+// >= 64 (their window, the 16 or 64 bytes ending at the packet end, lies in the view).
+__device__ __forceinline__ bool ps_small(uint32_t off, uint32_t len) { return len <= kPsMaxLen && off >= kPsMinOff; }
+// low 32 bits of 0xFFFFFFFF << clamp(t, 0, 32): keeps the bytes at and above t / 8
+__device__ __forceinline__ uint32_t keep_from(int32_t t) {
+    const int32_t c = t < 0 ? 0 : (t > 32 ? 32 : t);
+    return uint32_t(uint64_t(0xFFFFFFFFu) << uint32_t(c));
+}
+// Inclusive prefix max over the wave with DPP (as wave_incl_add).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false)));
+    return v;
+}
 static_assert(kPcThreads >= 128 && kPcThreads <= 1024 && (kPcThreads & (kPcThreads - 1)) == 0, "k_pieces block");
 struct WaveSplit {
     static constexpr uint32_t kReg = 8, kThreads = kPcThreads, kWaves = kThreads / 64;
@@ -815,7 +847,7 @@ struct WaveSplit {
         uint32_t k[kReg], sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) {
-            k[j] = j < m ? pieces_of_len(prov.len_of(raw[j])) : 0u;
+            k[j] = j < m ? split_pieces<Prov>(prov.len_of(raw[j])) : 0u;
             sum += k[j];
         }
         for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p);  // > kReg per thread
@@ -837,6 +869,12 @@ struct WaveSplit {
             total += v;
         }
         const uint32_t excl = before + incl - sum;
+        if (total == 0 && threadIdx.x == 0) {  // no piece in the workgroup (all small): every wave empty
+            for (uint32_t w = 0; w <= nw; ++w) {
+                starts[w] = g1;
+                spre[w] = 0;
+            }
+        }
         for (uint32_t w = 1; w < nw; ++w) {
             const uint32_t target = uint32_t((uint64_t(total) * w) >> (kPcLogT - 6));
             if (target >= excl && target - excl < sum) {
@@ -853,7 +891,7 @@ struct WaveSplit {
                 spre[w] = pre;
             }
         }
-        if (threadIdx.x == 0) spre[nw] = total;
+        if (threadIdx.x == 0 && total != 0) spre[nw] = total;
         __syncthreads();
         lo = uniform64(starts[wave]);
         hi = uniform64(starts[wave + 1]);
@@ -930,29 +968,47 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         bool valid;
         prov.decode(raw, off, len, valid, aux, oslot);
         const bool have = p0 + lane < hi;
+        // small packets were done by the small-packet phase: 0 pieces here
+        const bool sm = Prov::kSmall && have && ps_small(uint32_t(off), len);
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
             len = 0;
             valid = false;
         }
-        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 64u;
+        const uint32_t k = have ? (sm ? 0u : (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS)) : 64u;
         const uint32_t kr = k - (lane == 0 ? skip : 0u);  // pieces still to do
         const uint32_t incl = wave_incl_add(kr);
         const uint32_t excl = incl - kr;
         const uint32_t navail = __popcll(__ballot(have));  // packets of the wave left in view
         const uint32_t covered = uint32_t(__builtin_amdgcn_readlane(int(incl), int(navail - 1)));  // pieces in view
+        if (Prov::kSmall && covered == 0) {  // only small packets in view (wave-uniform)
+            p0 += navail;
+            meta(p0);
+            continue;
+        }
 
         // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
-        // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
+        // pk = (# flagged lanes <= this lane) - 1 from a ballot; with small packets (0
+        // pieces) in view, the first lane of a packet holds the packet's lane instead and
+        // pk is the prefix max -----------------------------------------------------------
         lu8 *const flags = (lu8 *)lds + kPcFlags + wave * 64u;
-        flags[lane] = 0;
-        if (have && excl < 64u) flags[excl] = 1;
-        __builtin_amdgcn_wave_barrier();
-        const bool start = flags[lane] != 0;
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t starts = __ballot(start);
-        uint32_t pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
-                      (start ? 1u : 0u) - 1u;
+        uint32_t pk;
+        if constexpr (Prov::kSmall) {
+            flags[lane] = 0;
+            if (have && kr > 0u && excl < 64u) flags[excl] = uint8_t(lane);
+            __builtin_amdgcn_wave_barrier();
+            pk = wave_incl_max(flags[lane]);
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            flags[lane] = 0;
+            if (have && excl < 64u) flags[excl] = 1;
+            __builtin_amdgcn_wave_barrier();
+            const bool start = flags[lane] != 0;
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t starts = __ballot(start);
+            pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
+                 (start ? 1u : 0u) - 1u;
+        }
         const bool mapped = lane < covered;
         pk = mapped ? pk : 0;
         const uint32_t pex = __shfl(excl, pk);
@@ -1126,11 +1182,137 @@ struct PcTables {
     }
 };
 
+// ---- small-packet phase (offset/length arrays) ------------------------------------------
+// C5 has 69% of its packets at <= 64 B; in the piece stream each takes a whole 64-B lane
+// (and its share of a round's mapping, rotation and scan).  Before the piece loop, the
+// workgroup classifies its packets in passes of kPsChunk: small ones (ps_small) are
+// compacted (LDS atomics) into the staging slots as {end, rel << 8 | len}, then finished
+// one lane per packet in rounds of 64 spread over the waves: the window of 16 B (len <=
+// 16) or 64 B ending at the packet end is one or four unaligned 16-B loads (in the view:
+// the packet starts at >= 64), bytes before the packet are masked, the slice-by-4 chain
+// gives R_0(window) = R_0(packet), crc = R_0 ^ shift(~0, len) ^ ~0 (head-init table).
+// The piece loop then skips them (0 pieces).
+constexpr uint32_t kPsChunk = 4096;                            // packets per pass: 32 KiB of entries
+constexpr uint32_t kPsCtl = (kPcLdsWords * 4 + 15) & ~15u;     // counters (T, M) x pass parity
+static_assert(kPcStage + kPsChunk * 8 <= kPcFlags && kPsCtl + 16 <= 163840, "small-phase LDS");
+constexpr uint32_t kPsGrp = kPsChunk / kPcThreads;             // packets per thread and pass
+
+template <class Prov>
+struct SmallMeta {  // one pass's metadata: packet g0 + c0 + k * kPcThreads + threadIdx.x
+    uint32_t o[kPsGrp], l[kPsGrp];
+    __device__ __forceinline__ void load(const Prov &prov, uint64_t c0, uint64_t n) {
+        const __amdgpu_buffer_rsrc_t ro = make_rsrc(prov.off_array(), uint32_t(8 * n));
+        const __amdgpu_buffer_rsrc_t rl = make_rsrc(prov.len_array(), uint32_t(4 * n));
+#pragma unroll
+        for (uint32_t k = 0; k < kPsGrp; ++k) {
+            const uint64_t p = c0 + k * kPcThreads + threadIdx.x;
+            o[k] = __builtin_amdgcn_raw_buffer_load_b32(ro, p < n ? int(8 * p) : int(0x80000000u), 0, 0);
+            l[k] = __builtin_amdgcn_raw_buffer_load_b32(rl, p < n ? int(4 * p) : int(0x80000000u), 0, 0);
+        }
+    }
+};
+
+template <class Prov, class Epi>
+__device__ __forceinline__ void small_phase(char *lds, __amdgpu_buffer_rsrc_t rs, const Prov &prov, const Epi &epi,
+                                            uint64_t g0, uint64_t g1, uint64_t n, SmallMeta<Prov> &sm,
+                                            uint32_t wave, uint32_t lane) {
+    const StagKeys K(lane);
+    lu32 *const ctl = (lu32 *)((lchar *)lds + kPsCtl);
+    lu32x2 *const ent = (lu32x2 *)((lchar *)lds + kPcStage);
+    const lu32 *const hinit = (const lu32 *)((lchar *)lds + kPcHinit);
+    const uint32_t nw = kPcThreads / 64;
+    uint32_t par = 0;
+    for (uint64_t c0 = g0; c0 < g1; c0 += kPsChunk, par ^= 1u) {
+        const uint64_t c1 = g1 - c0 < kPsChunk ? g1 : c0 + kPsChunk;
+        lu32 *const cnt = ctl + 2u * par;
+#pragma unroll
+        for (uint32_t k = 0; k < kPsGrp; ++k) {
+            const uint32_t rel = k * kPcThreads + threadIdx.x;
+            const uint32_t off = prov.view_lead() + sm.o[k], len = sm.l[k];
+            const bool small = c0 + rel < c1 && ps_small(off, len);
+            const uint64_t bT = __ballot(small && len <= 16), bM = __ballot(small && len > 16);
+            uint32_t baseT = 0, baseM = 0;
+            if (lane == 0) {
+                if (bT) baseT = __hip_atomic_fetch_add(&cnt[0], uint32_t(__popcll(bT)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (bM) baseM = __hip_atomic_fetch_add(&cnt[1], uint32_t(__popcll(bM)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            baseT = __builtin_amdgcn_readfirstlane(baseT);
+            baseM = __builtin_amdgcn_readfirstlane(baseM);
+            const uint64_t mine = len <= 16 ? bT : bM;
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi(uint32_t(mine >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mine), 0u));
+            if (small) ent[len <= 16 ? baseT + pos : kPsChunk - 1u - (baseM + pos)] = u32x2{off + len, (rel << 8) | len};
+        }
+        const uint64_t cn = c0 + kPsChunk;
+        if (cn < g1) sm.load(prov, cn, n);  // the next pass's metadata flies during the rounds
+        __syncthreads();
+        const uint32_t nT = __builtin_amdgcn_readfirstlane(cnt[0]), nM = __builtin_amdgcn_readfirstlane(cnt[1]);
+        if (threadIdx.x == 0) {  // the other parity's counters: last read before this barrier
+            ctl[2u * (par ^ 1u)] = 0;
+            ctl[2u * (par ^ 1u) + 1u] = 0;
+        }
+        const uint32_t rT = (nT + 63u) >> 6, rtot = (WTP_PS_DIAG & 1) ? 0u : rT + ((nM + 63u) >> 6);
+        struct SRound {
+            u32x4 x[4];
+            uint32_t len, rel;
+            bool on;
+        };
+        auto issue = [&](uint32_t r, SRound &S) {
+            const bool t = r < rT;
+            const uint32_t i = (t ? r : r - rT) * 64u + lane;
+            S.on = r < rtot && i < (t ? nT : nM);
+            const u32x2 e = ent[S.on ? (t ? i : kPsChunk - 1u - i) : 0u];
+            S.len = e.y & 0xFFu;
+            S.rel = e.y >> 8;
+            const uint32_t w0 = e.x - (t ? 16u : 64u);
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const bool ld = S.on && (u == 0 || !t);
+                S.x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rs, ld ? int(w0 + 16u * u) : int(0x80000000u), 0, 0));
+            }
+        };
+        auto compute = [&](uint32_t r, const SRound &S) {
+            uint32_t c = 0;
+            if (r < rT) {  // 16-B window, vf = 16 - len bytes before the packet
+                const int32_t vf8 = 8 * int32_t(16u - S.len);
+                const uint32_t w[4] = {S.x[0].x, S.x[0].y, S.x[0].z, S.x[0].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (w[i] & keep_from(vf8 - 32 * i)));
+            } else {  // 64-B window
+                const int32_t vf8 = 8 * int32_t(64u - S.len);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t w[4] = {S.x[u].x, S.x[u].y, S.x[u].z, S.x[u].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (w[i] & keep_from(vf8 - 32 * (4 * u + i))));
+                }
+            }
+            epi.put(c0 + S.rel, c ^ hinit[S.len] ^ 0xFFFFFFFFu, true, 0u, S.on);
+        };
+        {
+            SRound A, B;
+            uint32_t r = wave;
+            issue(r, A);
+            while (r < rtot) {
+                issue(r + nw, B);
+                compute(r, A);
+                r += nw;
+                if (r >= rtot) break;
+                issue(r + nw, A);
+                compute(r, B);
+                r += nw;
+            }
+        }
+        __syncthreads();  // the entries are dead: the next pass (or the piece loop) reuses the slots
+    }
+}
+
 template <class Prov, class Epi>
 __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
                                                  uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
                                                  uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[(kPsCtl + 16) / 4];  // + the small phase's counters
     char *lds = reinterpret_cast<char *>(lds_w);
     const uint32_t nw = blockDim.x >> 6;
     const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
@@ -1148,8 +1330,13 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     // neutral on C5, 53.4 vs 52.9 us back to back, profiles/r03f/abc5.log.)
     tb.load(gtab);
     if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
+    SmallMeta<Prov> smeta;
+    if constexpr (Prov::kSmall) smeta.load(prov, g0, n);
     PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
     tb.store(lds, gtab);
+    if constexpr (Prov::kSmall) {
+        if (threadIdx.x < 4) reinterpret_cast<lu32 *>((lchar *)lds + kPsCtl)[threadIdx.x] = 0;
+    }
     uint64_t lo, hi;
     uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
     if constexpr (Prov::kVarLen) {
@@ -1162,6 +1349,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     if (lo < hi) pieces_meta(prov, lo, hi, lane, raw, rs);
     __syncthreads();  // the tables are visible to every wave
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
+    if constexpr (Prov::kSmall && !(WTP_PS_DIAG & 2)) small_phase(lds, rs, prov, epi, g0, g1, n, smeta, wave, lane);
 
     pieces_loop(lds, rs, prov, epi, lo, hi, wpieces, status, wave, lane, raw);
 }
@@ -1193,12 +1381,12 @@ constexpr uint32_t kVfPer = 8;                          // packets rescanned per
 constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
 static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fix-up LDS");
 
-typedef __attribute__((address_space(3))) uint32_t lu32;
 
 // Datagram list[p] of the ring (lead 0: the ring is 16-B aligned); aux = ntohl(checksum).
 struct LdsIdxDgramProv {
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
+    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride;
     const uint32_t *__restrict__ rl;
     const lu32 *list;
@@ -1335,11 +1523,6 @@ constexpr uint32_t kBvNoPkt = 0xFFFFFFFFu;
 #define WTP_BV_DIAG 0  // ablation builds only (wrong CRCs): 1 no phase-B rounds, 2 no phase-S rounds, 4 phase B without hashing
 #endif
 
-// low 32 bits of 0xFFFFFFFF << clamp(t, 0, 32): keeps the bytes at and above t / 8
-__device__ __forceinline__ uint32_t keep_from(int32_t t) {
-    const int32_t c = t < 0 ? 0 : (t > 32 ? 32 : t);
-    return uint32_t(uint64_t(0xFFFFFFFFu) << uint32_t(c));
-}
 // dword w at view offset a of a packet starting at `off`: bytes before the packet are
 // zeroed, the packet's first 4 bytes complemented (the CRC's ~0 initial value)
 __device__ __forceinline__ uint32_t head_word(uint32_t w, int32_t u) {  // u = off - a
@@ -1352,6 +1535,7 @@ __device__ __forceinline__ uint32_t head_word(uint32_t w, int32_t u) {  // u = o
 struct LdsIdxArrayProv {
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
+    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     const uint32_t *__restrict__ offs;  // low dwords of the u64 offsets (view < 2 GiB)
     const uint32_t *__restrict__ lens;
     uint32_t lead;
@@ -2396,6 +2580,7 @@ namespace dev {
 struct FixedProvL {
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride, lead;
     uint32_t len;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
@@ -2409,6 +2594,7 @@ struct FixedProvL {
 struct ArrayProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kSmall = WTP_PC_SMALL;  // see k_pieces' small-packet phase
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
@@ -2418,6 +2604,8 @@ struct ArrayProvL {
     }
     __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
     __device__ __forceinline__ const uint32_t *len_array() const { return lens; }
+    __device__ __forceinline__ const uint32_t *off_array() const { return reinterpret_cast<const uint32_t *>(offs); }
+    __device__ __forceinline__ uint32_t view_lead() const { return uint32_t(lead); }
     __device__ __forceinline__ uint32_t len_of(uint32_t w) const { return w; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
                                            uint32_t &) const {
@@ -2434,6 +2622,7 @@ struct ArrayProvL {
 struct DgramProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
