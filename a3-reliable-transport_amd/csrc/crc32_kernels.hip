@@ -53,7 +53,6 @@ constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
 constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
 constexpr int kPieceS = 64;                  // piece bytes in the general kernel
 constexpr uint32_t kMaxVarLen = 4096;
-constexpr uint32_t kPsMaxLen = 64, kPsMinOff = 64;  // k_pieces' small packets (ps_small)
 constexpr uint64_t kSubBatch = 1ull << 28;      // packets per general-kernel launch (32-bit store offsets)        // 64 pieces x 64 B: one packet per wave max
 
 constexpr uint32_t OFF_BRAID = 0;            // 4x256 braid word tables (advance 256 B)
@@ -91,7 +90,6 @@ typedef __attribute__((address_space(3))) char lchar;
 typedef __attribute__((address_space(3))) u32x4 lu32x4;
 typedef __attribute__((address_space(3))) u32x2 lu32x2;
 typedef __attribute__((address_space(3))) uint8_t lu8;
-typedef __attribute__((address_space(3))) uint32_t lu32;
 
 // Per-wave phase timestamps for tools/pprobe.hip (built with -DWTP_PROBE=1 there and
 // compiled out of the product): slot k of wave (block, wave) gets value v, e.g. a
@@ -759,15 +757,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 __device__ __forceinline__ uint32_t pieces_of_len(uint32_t len) {
     return (len == 0 || len > kMaxVarLen) ? 1u : (len + kPieceS - 1) / kPieceS;
 }
-// pieces a packet takes in the piece stream (the wave split's estimate: small packets,
-// done by the small-packet phase, count 0 whatever their offset)
-template <class Prov>
-__device__ __forceinline__ uint32_t split_pieces(uint32_t len) {
-    return (Prov::kSmall && len <= kPsMaxLen) ? 0u : pieces_of_len(len);
-}
 template <class Prov>
 __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
-    return split_pieces<Prov>(prov.len_of(prov.load_len(p)));
+    return pieces_of_len(prov.len_of(prov.load_len(p)));
 }
 
 // Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
@@ -790,30 +782,6 @@ constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThrea
 #ifndef WTP_PC_LAG
 #define WTP_PC_LAG 1  // k_pieces: wave priority by work left (0: rotate by round and age)
 #endif
-#ifndef WTP_PC_SMALL
-#define WTP_PC_SMALL 0  // k_pieces, offset/length arrays: small-packet phase (measured slower; 1: A/B builds)
-#endif
-#ifndef WTP_PS_DIAG
-#define WTP_PS_DIAG 0  // ablation builds only (wrong CRCs): 1 no small rounds, 2 no small phase at all (the piece loop still skips)
-#endif
-// Small packets (k_pieces' small-packet phase): 0 <= len <= 64 and starting at view offset
-// >= 64 (their window, the 16 or 64 bytes ending at the packet end, lies in the view).
-__device__ __forceinline__ bool ps_small(uint32_t off, uint32_t len) { return len <= kPsMaxLen && off >= kPsMinOff; }
-// low 32 bits of 0xFFFFFFFF << clamp(t, 0, 32): keeps the bytes at and above t / 8
-__device__ __forceinline__ uint32_t keep_from(int32_t t) {
-    const int32_t c = t < 0 ? 0 : (t > 32 ? 32 : t);
-    return uint32_t(uint64_t(0xFFFFFFFFu) << uint32_t(c));
-}
-// Inclusive prefix max over the wave with DPP (as wave_incl_add).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false)));
-    return v;
-}
 static_assert(kPcThreads >= 128 && kPcThreads <= 1024 && (kPcThreads & (kPcThreads - 1)) == 0, "k_pieces block");
 struct WaveSplit {
     static constexpr uint32_t kReg = 8, kThreads = kPcThreads, kWaves = kThreads / 64;
@@ -847,7 +815,7 @@ struct WaveSplit {
         uint32_t k[kReg], sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) {
-            k[j] = j < m ? split_pieces<Prov>(prov.len_of(raw[j])) : 0u;
+            k[j] = j < m ? pieces_of_len(prov.len_of(raw[j])) : 0u;
             sum += k[j];
         }
         for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p);  // > kReg per thread
@@ -869,12 +837,6 @@ struct WaveSplit {
             total += v;
         }
         const uint32_t excl = before + incl - sum;
-        if (total == 0 && threadIdx.x == 0) {  // no piece in the workgroup (all small): every wave empty
-            for (uint32_t w = 0; w <= nw; ++w) {
-                starts[w] = g1;
-                spre[w] = 0;
-            }
-        }
         for (uint32_t w = 1; w < nw; ++w) {
             const uint32_t target = uint32_t((uint64_t(total) * w) >> (kPcLogT - 6));
             if (target >= excl && target - excl < sum) {
@@ -891,7 +853,7 @@ struct WaveSplit {
                 spre[w] = pre;
             }
         }
-        if (threadIdx.x == 0 && total != 0) spre[nw] = total;
+        if (threadIdx.x == 0) spre[nw] = total;
         __syncthreads();
         lo = uniform64(starts[wave]);
         hi = uniform64(starts[wave + 1]);
@@ -968,47 +930,29 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         bool valid;
         prov.decode(raw, off, len, valid, aux, oslot);
         const bool have = p0 + lane < hi;
-        // small packets were done by the small-packet phase: 0 pieces here
-        const bool sm = Prov::kSmall && have && ps_small(uint32_t(off), len);
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
             len = 0;
             valid = false;
         }
-        const uint32_t k = have ? (sm ? 0u : (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS)) : 64u;
+        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 64u;
         const uint32_t kr = k - (lane == 0 ? skip : 0u);  // pieces still to do
         const uint32_t incl = wave_incl_add(kr);
         const uint32_t excl = incl - kr;
         const uint32_t navail = __popcll(__ballot(have));  // packets of the wave left in view
         const uint32_t covered = uint32_t(__builtin_amdgcn_readlane(int(incl), int(navail - 1)));  // pieces in view
-        if (Prov::kSmall && covered == 0) {  // only small packets in view (wave-uniform)
-            p0 += navail;
-            meta(p0);
-            continue;
-        }
 
         // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
-        // pk = (# flagged lanes <= this lane) - 1 from a ballot; with small packets (0
-        // pieces) in view, the first lane of a packet holds the packet's lane instead and
-        // pk is the prefix max -----------------------------------------------------------
+        // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
         lu8 *const flags = (lu8 *)lds + kPcFlags + wave * 64u;
-        uint32_t pk;
-        if constexpr (Prov::kSmall) {
-            flags[lane] = 0;
-            if (have && kr > 0u && excl < 64u) flags[excl] = uint8_t(lane);
-            __builtin_amdgcn_wave_barrier();
-            pk = wave_incl_max(flags[lane]);
-            __builtin_amdgcn_wave_barrier();
-        } else {
-            flags[lane] = 0;
-            if (have && excl < 64u) flags[excl] = 1;
-            __builtin_amdgcn_wave_barrier();
-            const bool start = flags[lane] != 0;
-            __builtin_amdgcn_wave_barrier();
-            const uint64_t starts = __ballot(start);
-            pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
-                 (start ? 1u : 0u) - 1u;
-        }
+        flags[lane] = 0;
+        if (have && excl < 64u) flags[excl] = 1;
+        __builtin_amdgcn_wave_barrier();
+        const bool start = flags[lane] != 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t starts = __ballot(start);
+        uint32_t pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
+                      (start ? 1u : 0u) - 1u;
         const bool mapped = lane < covered;
         pk = mapped ? pk : 0;
         const uint32_t pex = __shfl(excl, pk);
@@ -1182,137 +1126,11 @@ struct PcTables {
     }
 };
 
-// ---- small-packet phase (offset/length arrays) ------------------------------------------
-// C5 has 69% of its packets at <= 64 B; in the piece stream each takes a whole 64-B lane
-// (and its share of a round's mapping, rotation and scan).  Before the piece loop, the
-// workgroup classifies its packets in passes of kPsChunk: small ones (ps_small) are
-// compacted (LDS atomics) into the staging slots as {end, rel << 8 | len}, then finished
-// one lane per packet in rounds of 64 spread over the waves: the window of 16 B (len <=
-// 16) or 64 B ending at the packet end is one or four unaligned 16-B loads (in the view:
-// the packet starts at >= 64), bytes before the packet are masked, the slice-by-4 chain
-// gives R_0(window) = R_0(packet), crc = R_0 ^ shift(~0, len) ^ ~0 (head-init table).
-// The piece loop then skips them (0 pieces).
-constexpr uint32_t kPsChunk = 4096;                            // packets per pass: 32 KiB of entries
-constexpr uint32_t kPsCtl = (kPcLdsWords * 4 + 15) & ~15u;     // counters (T, M) x pass parity
-static_assert(kPcStage + kPsChunk * 8 <= kPcFlags && kPsCtl + 16 <= 163840, "small-phase LDS");
-constexpr uint32_t kPsGrp = kPsChunk / kPcThreads;             // packets per thread and pass
-
-template <class Prov>
-struct SmallMeta {  // one pass's metadata: packet g0 + c0 + k * kPcThreads + threadIdx.x
-    uint32_t o[kPsGrp], l[kPsGrp];
-    __device__ __forceinline__ void load(const Prov &prov, uint64_t c0, uint64_t n) {
-        const __amdgpu_buffer_rsrc_t ro = make_rsrc(prov.off_array(), uint32_t(8 * n));
-        const __amdgpu_buffer_rsrc_t rl = make_rsrc(prov.len_array(), uint32_t(4 * n));
-#pragma unroll
-        for (uint32_t k = 0; k < kPsGrp; ++k) {
-            const uint64_t p = c0 + k * kPcThreads + threadIdx.x;
-            o[k] = __builtin_amdgcn_raw_buffer_load_b32(ro, p < n ? int(8 * p) : int(0x80000000u), 0, 0);
-            l[k] = __builtin_amdgcn_raw_buffer_load_b32(rl, p < n ? int(4 * p) : int(0x80000000u), 0, 0);
-        }
-    }
-};
-
-template <class Prov, class Epi>
-__device__ __forceinline__ void small_phase(char *lds, __amdgpu_buffer_rsrc_t rs, const Prov &prov, const Epi &epi,
-                                            uint64_t g0, uint64_t g1, uint64_t n, SmallMeta<Prov> &sm,
-                                            uint32_t wave, uint32_t lane) {
-    const StagKeys K(lane);
-    lu32 *const ctl = (lu32 *)((lchar *)lds + kPsCtl);
-    lu32x2 *const ent = (lu32x2 *)((lchar *)lds + kPcStage);
-    const lu32 *const hinit = (const lu32 *)((lchar *)lds + kPcHinit);
-    const uint32_t nw = kPcThreads / 64;
-    uint32_t par = 0;
-    for (uint64_t c0 = g0; c0 < g1; c0 += kPsChunk, par ^= 1u) {
-        const uint64_t c1 = g1 - c0 < kPsChunk ? g1 : c0 + kPsChunk;
-        lu32 *const cnt = ctl + 2u * par;
-#pragma unroll
-        for (uint32_t k = 0; k < kPsGrp; ++k) {
-            const uint32_t rel = k * kPcThreads + threadIdx.x;
-            const uint32_t off = prov.view_lead() + sm.o[k], len = sm.l[k];
-            const bool small = c0 + rel < c1 && ps_small(off, len);
-            const uint64_t bT = __ballot(small && len <= 16), bM = __ballot(small && len > 16);
-            uint32_t baseT = 0, baseM = 0;
-            if (lane == 0) {
-                if (bT) baseT = __hip_atomic_fetch_add(&cnt[0], uint32_t(__popcll(bT)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (bM) baseM = __hip_atomic_fetch_add(&cnt[1], uint32_t(__popcll(bM)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            baseT = __builtin_amdgcn_readfirstlane(baseT);
-            baseM = __builtin_amdgcn_readfirstlane(baseM);
-            const uint64_t mine = len <= 16 ? bT : bM;
-            const uint32_t pos = __builtin_amdgcn_mbcnt_hi(uint32_t(mine >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mine), 0u));
-            if (small) ent[len <= 16 ? baseT + pos : kPsChunk - 1u - (baseM + pos)] = u32x2{off + len, (rel << 8) | len};
-        }
-        const uint64_t cn = c0 + kPsChunk;
-        if (cn < g1) sm.load(prov, cn, n);  // the next pass's metadata flies during the rounds
-        __syncthreads();
-        const uint32_t nT = __builtin_amdgcn_readfirstlane(cnt[0]), nM = __builtin_amdgcn_readfirstlane(cnt[1]);
-        if (threadIdx.x == 0) {  // the other parity's counters: last read before this barrier
-            ctl[2u * (par ^ 1u)] = 0;
-            ctl[2u * (par ^ 1u) + 1u] = 0;
-        }
-        const uint32_t rT = (nT + 63u) >> 6, rtot = (WTP_PS_DIAG & 1) ? 0u : rT + ((nM + 63u) >> 6);
-        struct SRound {
-            u32x4 x[4];
-            uint32_t len, rel;
-            bool on;
-        };
-        auto issue = [&](uint32_t r, SRound &S) {
-            const bool t = r < rT;
-            const uint32_t i = (t ? r : r - rT) * 64u + lane;
-            S.on = r < rtot && i < (t ? nT : nM);
-            const u32x2 e = ent[S.on ? (t ? i : kPsChunk - 1u - i) : 0u];
-            S.len = e.y & 0xFFu;
-            S.rel = e.y >> 8;
-            const uint32_t w0 = e.x - (t ? 16u : 64u);
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const bool ld = S.on && (u == 0 || !t);
-                S.x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        rs, ld ? int(w0 + 16u * u) : int(0x80000000u), 0, 0));
-            }
-        };
-        auto compute = [&](uint32_t r, const SRound &S) {
-            uint32_t c = 0;
-            if (r < rT) {  // 16-B window, vf = 16 - len bytes before the packet
-                const int32_t vf8 = 8 * int32_t(16u - S.len);
-                const uint32_t w[4] = {S.x[0].x, S.x[0].y, S.x[0].z, S.x[0].w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (w[i] & keep_from(vf8 - 32 * i)));
-            } else {  // 64-B window
-                const int32_t vf8 = 8 * int32_t(64u - S.len);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t w[4] = {S.x[u].x, S.x[u].y, S.x[u].z, S.x[u].w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        c = stag_apply3<0>(lds, K.kA, K.sel, c ^ (w[i] & keep_from(vf8 - 32 * (4 * u + i))));
-                }
-            }
-            epi.put(c0 + S.rel, c ^ hinit[S.len] ^ 0xFFFFFFFFu, true, 0u, S.on);
-        };
-        {
-            SRound A, B;
-            uint32_t r = wave;
-            issue(r, A);
-            while (r < rtot) {
-                issue(r + nw, B);
-                compute(r, A);
-                r += nw;
-                if (r >= rtot) break;
-                issue(r + nw, A);
-                compute(r, B);
-                r += nw;
-            }
-        }
-        __syncthreads();  // the entries are dead: the next pass (or the piece loop) reuses the slots
-    }
-}
-
 template <class Prov, class Epi>
 __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
                                                  uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
                                                  uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[(kPsCtl + 16) / 4];  // + the small phase's counters
+    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
     const uint32_t nw = blockDim.x >> 6;
     const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
@@ -1330,13 +1148,8 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     // neutral on C5, 53.4 vs 52.9 us back to back, profiles/r03f/abc5.log.)
     tb.load(gtab);
     if constexpr (Prov::kVarLen) split.load(prov, g0, g1);
-    SmallMeta<Prov> smeta;
-    if constexpr (Prov::kSmall) smeta.load(prov, g0, n);
     PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
     tb.store(lds, gtab);
-    if constexpr (Prov::kSmall) {
-        if (threadIdx.x < 4) reinterpret_cast<lu32 *>((lchar *)lds + kPsCtl)[threadIdx.x] = 0;
-    }
     uint64_t lo, hi;
     uint32_t wpieces = 0;  // pieces of this wave's range (variable-length providers)
     if constexpr (Prov::kVarLen) {
@@ -1349,7 +1162,6 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
     if (lo < hi) pieces_meta(prov, lo, hi, lane, raw, rs);
     __syncthreads();  // the tables are visible to every wave
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
-    if constexpr (Prov::kSmall && !(WTP_PS_DIAG & 2)) small_phase(lds, rs, prov, epi, g0, g1, n, smeta, wave, lane);
 
     pieces_loop(lds, rs, prov, epi, lo, hi, wpieces, status, wave, lane, raw);
 }
@@ -1381,12 +1193,12 @@ constexpr uint32_t kVfPer = 8;                          // packets rescanned per
 constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
 static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fix-up LDS");
 
+typedef __attribute__((address_space(3))) uint32_t lu32;
 
 // Datagram list[p] of the ring (lead 0: the ring is 16-B aligned); aux = ntohl(checksum).
 struct LdsIdxDgramProv {
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
-    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride;
     const uint32_t *__restrict__ rl;
     const lu32 *list;
@@ -1474,476 +1286,6 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
         __syncthreads();  // the next pass rebuilds the list
     }
     if (threadIdx.x == 0 && found != total) __hip_atomic_fetch_or(st, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ------------------------------------------------------------------------------------
-// 2c. braided mixed-length kernel (k_braid_var): batches of any offsets and lengths
-// ------------------------------------------------------------------------------------
-// The piece stream (k_pieces) spends ~430 VALU instructions per 64-piece round: every
-// piece pays the window rotation, masking, lane mapping and a segmented scan, and every
-// packet takes at least one 64-B lane (C5: 69% of the packets are <= 64 B).  This kernel
-// sorts each workgroup's packets into three kinds (Crc32.hpp:91-102 for all of them):
-//   small  (len <= 64, 69% of C5's packets): one lane per packet, rounds of 64 packets
-//          compacted across the workgroup: the window (16 B for len <= 16, else 64 B)
-//          ending at the packet end is one (four) unaligned 16-B loads, bytes before the
-//          packet are masked, the words are combined backwards by Horner with x^-32 and
-//          moved to R_0 by x^(8 W) = T256 x^-1024 (x^-128)^k; crc = R_0 ^ shift(~0, len) ^ ~0;
-//   braided (64 < len <= 1536): k_fixed_braid's layout, 16 lanes per packet, 4 packets
-//          per wave round, but every frame is END-aligned to its packet (R = ceil(len /
-//          256) rows of 256 B, unaligned 16-B row loads), so no trailing-zero fix is
-//          needed; the frame bytes before the packet (row 0 only, when the 4 packets of
-//          the round have equal R) are masked, and the CRC's ~0 initial value is injected
-//          by complementing the packet's first 4 bytes (R_~0(P) = R_0(P ^ (FF^4 || 0...)));
-//          the braid loop, in-lane fold and Horner flush are the fixed kernel's, and
-//          they do not depend on R;
-//   odd    (len > 1536, or the packet starts in the view's first 64 B, where a window
-//          load would start before the buffer): finished at the end by the piece loop,
-//          like the verify fix-up (the workgroup rescans its packets into an LDS list).
-// Per workgroup: phase S classifies the packets in chunks of 2048 (entries compacted in
-// the transposition region, LDS atomics) and runs the small rounds; phase B claims
-// 64-packet groups (LDS counter), sorts each group's braided packets by R into a per-wave
-// buffer and runs their rounds through a 3-deep register pipeline (two rounds of loads in
-// flight while one is hashed; 8 waves per CU, the tables fill the LDS).
-constexpr uint32_t kBvThreads = 512, kBvWaves = kBvThreads / 64;
-constexpr uint32_t kBvMaxLen = 1536;  // braided: 64 < len <= 1536 (6 rows)
-constexpr uint32_t kBvSmall = 64;     // small: len <= 64
-constexpr uint32_t kBvMinOff = 64;    // packets starting before view offset 64: fix-up
-constexpr uint32_t kBvChunk = 2048;   // packets per phase-S pass (8-B entries, 16 KiB)
-constexpr uint32_t kBvXpose = kBraidXpose;                 // 8 x 2 KiB (phase S: entries)
-constexpr uint32_t kBvGrp = kBvXpose + kBvWaves * 2048;    // per wave 2 x 64 x 8 B
-constexpr uint32_t kBvFin = kBvGrp + kBvWaves * 1024;      // per wave 32 x {p, len}
-constexpr uint32_t kBvHinit = kBvFin + kBvWaves * 256;     // shift(~0, h), h = 0..64
-constexpr uint32_t kBvCtl = kBvHinit + 272;                // control words
-static_assert(kBvCtl + 64 <= kBraidLdsWords * 4 && kBvChunk * 8 == kBvWaves * 2048, "k_braid_var LDS");
-static_assert(kVfWaves == kBvWaves, "fix-up layout");
-// control words: [0..3] phase-S counters (T, M) of even / odd chunks, [4] phase-B group
-// claims, [5] odd packets counted by phase S
-constexpr uint32_t kBvNoPkt = 0xFFFFFFFFu;
-#ifndef WTP_BV_DIAG
-#define WTP_BV_DIAG 0  // ablation builds only (wrong CRCs): 1 no phase-B rounds, 2 no phase-S rounds, 4 phase B without hashing
-#endif
-
-// dword w at view offset a of a packet starting at `off`: bytes before the packet are
-// zeroed, the packet's first 4 bytes complemented (the CRC's ~0 initial value)
-__device__ __forceinline__ uint32_t head_word(uint32_t w, int32_t u) {  // u = off - a
-    const uint32_t keep = keep_from(8 * u), ninj = keep_from(8 * u + 32);
-    return keep & ~(w ^ ninj);
-}
-
-// Packet p of an array batch as the odd-packet fix-up's piece loop reads it: list[] holds
-// packet indices (kIndexed: the output slot is the packet index).
-struct LdsIdxArrayProv {
-    static constexpr bool kVarLen = false;
-    static constexpr bool kIndexed = true;
-    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
-    const uint32_t *__restrict__ offs;  // low dwords of the u64 offsets (view < 2 GiB)
-    const uint32_t *__restrict__ lens;
-    uint32_t lead;
-    const lu32 *list;
-    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
-        const uint32_t idx = list[p];
-        r.a = idx;
-        r.b = offs[2 * uint64_t(idx)];
-        r.c = lens[idx];
-    }
-    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
-                                           uint32_t &slot) const {
-        off = uint64_t(lead) + r.b;
-        l = r.c;
-        ok = true;
-        slot = uint32_t(r.a);
-    }
-};
-
-template <class Epi>
-__global__ __launch_bounds__(kBvThreads) void k_braid_var(const uint8_t *__restrict__ base, uint32_t nbytes,
-                                                          const uint64_t *__restrict__ offs64,
-                                                          const uint32_t *__restrict__ lens, uint32_t lead, uint64_t n,
-                                                          Epi epi, const uint32_t *__restrict__ gtab,
-                                                          uint32_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];
-    char *lds = reinterpret_cast<char *>(lds_w);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t g0 = n * blockIdx.x / gridDim.x, g1 = n * (blockIdx.x + 1) / gridDim.x;
-    if (g0 == g1) return;
-    const uint32_t *const offs = reinterpret_cast<const uint32_t *>(offs64);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, nbytes);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(offs, uint32_t(8 * n));  // n < 2^28
-    const __amdgpu_buffer_rsrc_t rl = make_rsrc(lens, uint32_t(4 * n));
-    const StagKeys K(lane);
-    lu32 *const ctl = (lu32 *)((lchar *)lds + kBvCtl);
-    lu32 *const hinit = (lu32 *)((lchar *)lds + kBvHinit);
-    // metadata of packet p: (view offset, length); p >= n reads (lead, 0)
-    auto meta_ld = [&](uint64_t p, uint32_t &o, uint32_t &l) {
-        const bool in = p < n;
-        o = __builtin_amdgcn_raw_buffer_load_b32(ro, in ? int(8 * p) : int(0x80000000u), 0, 0);
-        l = __builtin_amdgcn_raw_buffer_load_b32(rl, in ? int(4 * p) : int(0x80000000u), 0, 0);
-    };
-    auto is_odd = [&](uint32_t off, uint32_t len) { return len > kBvMaxLen || off < kBvMinOff; };
-
-    // ---- prologue: tables (region A: braid T256, x^-32; region B: x^-128, x^-1024), the
-    // head-init table, and chunk 0's metadata, all loads first ------------------------------
-    const StagSet sets[4] = {{gtab + OFF_BRAID, 0u},
-                             {gtab + OFF_INV + 0 * 1024, 128u},
-                             {gtab + OFF_INV + 2 * 1024, 65536u},
-                             {gtab + OFF_INV + 5 * 1024, 65536u + 128u}};
-    StagFill<4, kBvThreads> fill;
-    fill.load(sets);
-    const uint32_t hv = gtab[OFF_HINIT + (threadIdx.x <= kBvSmall ? threadIdx.x : 0u)];
-    constexpr uint32_t kGrpPerWave = kBvChunk / 64 / kBvWaves;  // 4
-    uint32_t mo[kGrpPerWave], ml[kGrpPerWave];
-    auto chunk_meta = [&](uint64_t c0) {
-#pragma unroll
-        for (uint32_t k = 0; k < kGrpPerWave; ++k) meta_ld(c0 + 64u * (wave + kBvWaves * k) + lane, mo[k], ml[k]);
-    };
-    chunk_meta(g0);
-    fill.store(lds, sets);
-    if (threadIdx.x <= kBvSmall) hinit[threadIdx.x] = hv;
-    if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
-    __syncthreads();
-
-    // ---- phase S: small packets --------------------------------------------------------
-    lu32x2 *const sent = (lu32x2 *)((lchar *)lds + kBvXpose);  // [kBvChunk] {end, rel << 8 | len}
-    uint32_t ci = 0;
-    for (uint64_t c0 = g0; c0 < g1; c0 += kBvChunk, ++ci) {
-        const uint64_t c1 = g1 - c0 < kBvChunk ? g1 : c0 + kBvChunk;
-        lu32 *const cnt = ctl + 2u * (ci & 1u);
-#pragma unroll
-        for (uint32_t k = 0; k < kGrpPerWave; ++k) {
-            const uint32_t rel = 64u * (wave + kBvWaves * k) + lane;
-            const bool have = c0 + rel < c1;
-            const uint32_t off = lead + mo[k], len = ml[k];
-            const bool odd = have && is_odd(off, len);
-            const bool sm = have && !odd && len <= kBvSmall;
-            const uint64_t bT = __ballot(sm && len <= 16), bM = __ballot(sm && len > 16), bO = __ballot(odd);
-            uint32_t baseT = 0, baseM = 0;
-            if (lane == 0) {
-                if (bT) baseT = __hip_atomic_fetch_add(&cnt[0], uint32_t(__popcll(bT)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (bM) baseM = __hip_atomic_fetch_add(&cnt[1], uint32_t(__popcll(bM)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (bO) __hip_atomic_fetch_add(&ctl[5], uint32_t(__popcll(bO)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            baseT = __builtin_amdgcn_readfirstlane(baseT);
-            baseM = __builtin_amdgcn_readfirstlane(baseM);
-            const uint64_t mine = sm && len <= 16 ? bT : bM;
-            const uint32_t pos = __builtin_amdgcn_mbcnt_hi(uint32_t(mine >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mine), 0u));
-            if (sm) {
-                const uint32_t slot = len <= 16 ? baseT + pos : kBvChunk - 1u - (baseM + pos);
-                sent[slot] = u32x2{off + len, (rel << 8) | len};
-            }
-        }
-        const uint64_t cn0 = c0 + kBvChunk;
-        if (cn0 < g1) chunk_meta(cn0);  // the next chunk's metadata flies during the rounds
-        __syncthreads();
-        const uint32_t nT = __builtin_amdgcn_readfirstlane(cnt[0]), nM = __builtin_amdgcn_readfirstlane(cnt[1]);
-        if (threadIdx.x == 0) {  // the other parity's counters: last read before this barrier
-            ctl[2u * ((ci + 1u) & 1u)] = 0;
-            ctl[2u * ((ci + 1u) & 1u) + 1u] = 0;
-        }
-        const uint32_t rT = (nT + 63u) >> 6, rM = (nM + 63u) >> 6, rtot = (WTP_BV_DIAG & 2) ? 0u : rT + rM;
-        // round r: T rounds first (entries from the front), then M rounds (from the back)
-        struct SRound {
-            u32x4 x[4];
-            uint32_t len, rel;
-            bool on;
-        };
-        auto s_issue = [&](uint32_t r, SRound &S) {
-            const bool t = r < rT;
-            const uint32_t i = (t ? r : r - rT) * 64u + lane;
-            S.on = r < rtot && i < (t ? nT : nM);
-            const u32x2 e = S.on ? sent[t ? i : kBvChunk - 1u - i] : u32x2{0u, 0u};
-            S.len = e.y & 0xFFu;
-            S.rel = e.y >> 8;
-            const uint32_t w0 = e.x - (t ? 16u : 64u);  // >= 0: the packet starts at >= 64
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const bool ld = S.on && (u == 0 || !t);
-                S.x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        rs, ld ? int(w0 + 16u * u) : int(0x80000000u), 0, 0));
-            }
-        };
-        auto s_compute = [&](uint32_t r, const SRound &S) {
-            uint32_t acc;
-            if (r < rT) {  // 16-B window: words w0..w3, vf = 16 - len bytes masked
-                const int32_t vf8 = 8 * int32_t(16u - S.len);
-                const uint32_t w[4] = {S.x[0].x, S.x[0].y, S.x[0].z, S.x[0].w};
-                acc = w[3] & keep_from(vf8 - 96);
-                acc = stag_apply3x<128>(lds, K.kA, K.sel, acc, w[2] & keep_from(vf8 - 64));
-                acc = stag_apply3x<128>(lds, K.kA, K.sel, acc, w[1] & keep_from(vf8 - 32));
-                acc = stag_apply3x<128>(lds, K.kA, K.sel, acc, w[0] & keep_from(vf8));
-#pragma unroll
-                for (int s = 0; s < 7; ++s) acc = stag_apply3<0>(lds, K.kB, K.sel, acc);  // x^-128
-            } else {  // 64-B window
-                const int32_t vf8 = 8 * int32_t(64u - S.len);
-                uint32_t w[16];
-#pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
-                    w[4 * u + 0] = S.x[u].x;
-                    w[4 * u + 1] = S.x[u].y;
-                    w[4 * u + 2] = S.x[u].z;
-                    w[4 * u + 3] = S.x[u].w;
-                }
-                acc = w[15] & keep_from(vf8 - 480);
-#pragma unroll
-                for (int i = 14; i >= 0; --i) acc = stag_apply3x<128>(lds, K.kA, K.sel, acc, w[i] & keep_from(vf8 - 32 * i));
-#pragma unroll
-                for (int s = 0; s < 4; ++s) acc = stag_apply3<0>(lds, K.kB, K.sel, acc);  // x^-128
-            }
-            acc = stag_apply3<128>(lds, K.kB, K.sel, acc);  // x^-1024
-            acc = stag_apply3<0>(lds, K.kA, K.sel, acc);    // T256: R_0 of the window
-            epi.put(c0 + S.rel, acc ^ hinit[S.len] ^ 0xFFFFFFFFu, true, 0u, S.on);
-        };
-        {
-            SRound A, B;
-            uint32_t r = wave;
-            s_issue(r, A);
-            while (r < rtot) {
-                s_issue(r + kBvWaves, B);
-                s_compute(r, A);
-                r += kBvWaves;
-                if (r >= rtot) break;
-                s_issue(r + kBvWaves, A);
-                s_compute(r, B);
-                r += kBvWaves;
-            }
-        }
-        __syncthreads();  // the entries are dead: the next chunk (or phase B) reuses the region
-    }
-
-    // ---- phase B: braided packets ------------------------------------------------------
-    const uint64_t ngroups = (WTP_BV_DIAG & 1) ? 0u : (g1 - g0 + 63u) >> 6;
-    lu32x2 *const gbuf = (lu32x2 *)((lchar *)lds + kBvGrp + wave * 1024u);  // [2][64] {end, len << 8 | lane}
-    lu32x2 *const fin = (lu32x2 *)((lchar *)lds + kBvFin + wave * 256u);    // [32] {p, len}
-    lchar *const xs = (lchar *)lds + kBvXpose + wave * 2048u;
-    const uint32_t j = lane & 15u, q = lane >> 4;
-    auto claim = [&]() {
-        uint32_t g = 0;
-        if (lane == 0) g = __hip_atomic_fetch_add(&ctl[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return uint64_t(__builtin_amdgcn_readfirstlane(g));
-    };
-    uint64_t gq = claim();  // the group whose metadata is in (qo, ql); lanes past g1 are not its
-    uint32_t qo, ql;
-    meta_ld(g0 + 64u * gq + lane, qo, ql);
-    uint32_t cb = 1, cs = 0, cn = 0;  // cursor: buffer, next entry, entries
-    uint64_t cgb = 0;                 // first packet of the buffered group
-    bool exhausted = false;
-
-    struct BRound {
-        u32x4 w[6];
-        uint32_t off, end;  // this lane's packet (view offsets)
-        uint32_t p, len;    // output index (kBvNoPkt: no packet), length
-        uint32_t rows;      // wave-uniform: 0 = empty round
-        uint32_t mixed;     // wave-uniform: rows differ within the round, or a head crosses into row 1
-        uint32_t done;      // wave-uniform: the workgroup's groups are exhausted (every later round is too)
-    };
-    // next round: 4 consecutive entries of the current buffer (sorted by rows, so the
-    // last one has the most); at the end of the buffer the prefetched group is sorted
-    // into the other buffer and the next group claimed (its metadata load flies while
-    // the buffered rounds run).  Every call issues the same 6 row loads (out of range:
-    // no traffic) so the loop's vmcnt accounting stays static.
-    auto b_issue = [&](BRound &X) {
-        // Explicit waits, so the compiler knows which loads are complete (it inserted
-        // vmcnt(0) here otherwise, reusing X's registers as temporaries): X's previous rows
-        // are older than the other two rounds' 12 row loads; the prefetched metadata is
-        // older than at least one round's 6.
-        __builtin_amdgcn_s_waitcnt(0x0F7C);  // vmcnt(12)
-        // at most one group switch per call (a loop here made the compiler copy the
-        // prefetched metadata registers, which waited for every load in flight); an empty
-        // group gives an empty round
-        if (!exhausted && cs >= cn) {
-            __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
-            if (gq >= ngroups) {
-                exhausted = true;
-            } else {
-                const uint32_t off = lead + qo, len = ql;
-                const bool br = g0 + 64u * gq + lane < g1 && !is_odd(off, len) && len > kBvSmall;
-                const uint32_t R = (len + 255u) >> 8;
-                lu32x2 *const dst = gbuf + 64u * (cb ^ 1u);
-                uint32_t nb = 0;
-#pragma unroll
-                for (uint32_t r = 1; r <= 6; ++r) {
-                    const uint64_t m = __ballot(br && R == r);
-                    const uint32_t pos = nb + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                    if (br && R == r) dst[pos] = u32x2{off + len, (len << 8) | lane};
-                    nb += uint32_t(__popcll(m));
-                }
-                cgb = g0 + 64u * gq;
-                cb ^= 1u;
-                cs = 0;
-                cn = nb;
-                gq = claim();
-                meta_ld(g0 + 64u * gq + lane, qo, ql);
-            }
-        }
-        X.done = exhausted ? 1u : 0u;
-        uint32_t R = 0, mixed = 0;
-        bool live = false;
-        X.off = 0;
-        X.end = 0;
-        X.p = kBvNoPkt;
-        X.len = 0;
-        if (!exhausted && cs < cn) {
-            const lu32x2 *const src = gbuf + 64u * cb;
-            const u32x2 el = src[cs + 3u < cn ? cs + 3u : cn - 1u], ef = src[cs];
-            R = __builtin_amdgcn_readfirstlane(((el.y >> 8) + 255u) >> 8);
-            const uint32_t Rf = __builtin_amdgcn_readfirstlane(((ef.y >> 8) + 255u) >> 8);
-            live = cs + q < cn;
-            const u32x2 e = src[live ? cs + q : cs];
-            if (live) {
-                X.end = e.x;
-                X.len = e.y >> 8;
-                X.off = e.x - X.len;
-                X.p = uint32_t(cgb) + (e.y & 0xFFu);
-            }
-            // the head's 4 injected bytes reach into row 1 when off - fs > 252
-            const bool cross = live && X.off - (X.end - 256u * R) > 252u;
-            mixed = (Rf != R || __ballot(cross) != 0) ? 1u : 0u;
-            cs += 4u;
-        }
-        X.rows = R;
-        X.mixed = mixed;
-        const uint32_t fs = X.end - 256u * R;
-#pragma unroll
-        for (uint32_t i = 0; i < 6; ++i) {
-            const uint32_t a = fs + 256u * i + 16u * j;
-            const bool ld = live && i < R && a + 16u > X.off;
-            if (i == 0)
-                X.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ld ? int(a) : int(0x80000000u), 0, 0));
-            else
-                X.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ld ? int(a) : int(0x80000000u), 0, 2));
-        }
-    };
-
-    uint32_t kk = 0;  // rounds in the transposition slot since the last flush
-    auto flush = [&]() {
-        __builtin_amdgcn_wave_barrier();
-        const u32x4 lo = *(const lu32x4 *)(xs + lane * 32u), hi = *(const lu32x4 *)(xs + lane * 32u + 16u);
-        uint32_t acc = hi.w;
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.y);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, hi.x);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.w);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.z);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.y);
-        acc = stag_apply3x<0>(lds, K.kB, K.sel, acc, lo.x);
-        const uint32_t h = lane & 1u;
-        {
-            const uint32_t y = stag_apply3<128>(lds, K.kB, K.sel, acc);  // x^-1024
-            acc = h ? y : acc;
-        }
-        acc ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(acc), 0xB1, 0xF, 0xF, false));  // lane ^ 1
-        acc = stag_apply3<0>(lds, K.kA, K.sel, acc);  // the deferred advance T past the last row
-        const u32x2 f = fin[lane >> 1];
-        const bool on = h == 0 && (lane >> 3) < kk && f.x != kBvNoPkt;
-        // the frame carried R_~0(packet) (initial value injected): crc = acc ^ ~0
-        epi.put(on ? f.x : 0u, acc ^ 0xFFFFFFFFu, true, 0u, on);
-        kk = 0;
-    };
-
-    auto b_compute = [&](const BRound &X) {
-        const uint32_t R = X.rows;
-        const uint32_t fs = X.end - 256u * R;
-        const int32_t u0 = int32_t(X.off - (fs + 16u * j));  // bytes of this lane's row-0 chunk before the packet
-        uint32_t b0 = head_word(X.w[0].x, u0), b1 = head_word(X.w[0].y, u0 - 4), b2 = head_word(X.w[0].z, u0 - 8),
-                 b3 = head_word(X.w[0].w, u0 - 12);
-#pragma unroll
-        for (uint32_t i = 1; i < 6; ++i) {
-            if (i < R) {  // wave-uniform
-                u32x4 w = X.w[i];
-                if (X.mixed) {  // rows before the packet or a head reaching into row 1
-                    const int32_t u = u0 - int32_t(256u * i);
-                    w.x = head_word(w.x, u);
-                    w.y = head_word(w.y, u - 4);
-                    w.z = head_word(w.z, u - 8);
-                    w.w = head_word(w.w, u - 12);
-                }
-                b0 = stag_apply3x<0>(lds, K.kA, K.sel, b0, w.x);
-                b1 = stag_apply3x<0>(lds, K.kA, K.sel, b1, w.y);
-                b2 = stag_apply3x<0>(lds, K.kA, K.sel, b2, w.z);
-                b3 = stag_apply3x<0>(lds, K.kA, K.sel, b3, w.w);
-            }
-        }
-        uint32_t v = stag_apply3x<128>(lds, K.kA, K.sel, b3, b2);
-        v = stag_apply3x<128>(lds, K.kA, K.sel, v, b1);
-        v = stag_apply3x<128>(lds, K.kA, K.sel, v, b0);
-        *(__attribute__((address_space(3))) uint32_t *)(xs + kk * 256u + lane * 4u) = v;
-        if (j == 0) fin[kk * 4u + q] = u32x2{X.p, X.len};
-        if (++kk == 8u) flush();
-    };
-
-    {
-        // the pipeline fills inside the loop (A and B start empty): no load is in flight at
-        // the loop entry that the back edge does not also have
-        BRound A, B, C;
-        A.rows = B.rows = 0;
-        A.done = B.done = 0;
-        // every row register counts as read once per round, computed or not (rows >= R and
-        // empty rounds hold zeros from out-of-range loads): otherwise a register of a
-        // skipped row is reused as a temporary while its load is still in flight, and the
-        // compiler waited for every load (vmcnt(0)) in the next issue
-        auto consume = [&](const BRound &X) {
-#pragma unroll
-            for (uint32_t i = 0; i < 6; ++i) __asm__ volatile("" ::"v"(X.w[i]));
-        };
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the loop entry then matches its back edge
-        for (;;) {
-            b_issue(C);
-            if (A.done) break;
-            if (A.rows && !(WTP_BV_DIAG & 4)) b_compute(A);
-            consume(A);
-            b_issue(A);
-            if (B.done) break;
-            if (B.rows && !(WTP_BV_DIAG & 4)) b_compute(B);
-            consume(B);
-            b_issue(B);
-            if (C.done) break;
-            if (C.rows && !(WTP_BV_DIAG & 4)) b_compute(C);
-            consume(C);
-        }
-        if (kk) flush();
-    }
-
-    // ---- odd packets: the piece loop over an LDS list (as the verify fix-up) -----------
-    __syncthreads();  // every wave is past phase B: the tables and buffers are dead
-    const uint32_t nodd = __builtin_amdgcn_readfirstlane(ctl[5]);
-    if (nodd == 0) return;
-    {
-        PcTables<kBvThreads> tb;  // overwrites the braid tables
-        tb.load(gtab);
-        tb.store(lds, gtab);
-    }
-    lu32 *const vctl = (lu32 *)((lchar *)lds + kVfCtl);
-    lu32 *const list = (lu32 *)((lchar *)lds + kVfList);
-    const LdsIdxArrayProv prov{offs, lens, lead, list};
-    uint32_t found = 0;
-    for (uint64_t e0 = g0; e0 < g1; e0 += kVfPass) {
-        if (threadIdx.x == 0) vctl[8] = 0;
-        __syncthreads();  // publishes the tables (first pass) and the reset list length
-        uint32_t ov[kVfPer], lv[kVfPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kVfPer; ++k) meta_ld(e0 + k * kBvThreads + threadIdx.x, ov[k], lv[k]);
-#pragma unroll
-        for (uint32_t k = 0; k < kVfPer; ++k) {
-            const uint64_t p = e0 + k * kBvThreads + threadIdx.x;
-            const bool need = p < g1 && is_odd(lead + ov[k], lv[k]);
-            const uint64_t m = __ballot(need);
-            if (m == 0) continue;  // wave-uniform
-            uint32_t b = 0;
-            if (lane == 0) b = __hip_atomic_fetch_add(&vctl[8], uint32_t(__popcll(m)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            b = __builtin_amdgcn_readfirstlane(b);
-            const uint32_t pos = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-            if (need) list[b + pos] = uint32_t(p);
-        }
-        __syncthreads();
-        const uint32_t c = __builtin_amdgcn_readfirstlane(vctl[8]);
-        found += c;
-        const uint64_t lo = uint64_t(c) * wave / kBvWaves, hi = uint64_t(c) * (wave + 1) / kBvWaves;
-        MetaRaw raw{};
-        if (lo < hi) pieces_meta(prov, lo, hi, lane, raw, rs);
-        pieces_loop(lds, rs, prov, epi, lo, hi, 0u, status, wave, lane, raw);
-        __syncthreads();  // the next pass rebuilds the list
-    }
-    if (threadIdx.x == 0 && found != nodd) __hip_atomic_fetch_or(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2537,24 +1879,6 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
     return launch_check("k_pieces");
 }
 
-// Mixed lengths below 2 GiB (k_braid_var): one workgroup per CU (its tables fill the
-// LDS), at least 256 packets per workgroup.
-template <class Epi>
-int launch_braid_var(DevState &s, const uint8_t *base, uint64_t nbytes, const uint64_t *offs, const uint32_t *lens,
-                     uint64_t n, Epi epi, hipStream_t st) {
-    const uintptr_t ub = reinterpret_cast<uintptr_t>(base);
-    const uint64_t lead = ub & 15u;
-    const uint8_t *b16 = base - lead;
-    const uint64_t span = (lead + nbytes + 15) & ~uint64_t(15);
-    if (span >= (1ull << 31)) return fail(WTP_EINVAL, "braided mixed-length span %llu B >= 2 GiB", (unsigned long long)span);
-    uint64_t grid = (n + 255) / 256;
-    if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((dev::k_braid_var<Epi>), dim3(unsigned(grid)), dim3(dev::kBvThreads), 0, st, b16, uint32_t(span),
-                       offs, lens, uint32_t(lead), n, epi, s.tabs, s.status);
-    return launch_check("k_braid_var");
-}
-
 // Packed mixed lengths (k_stream): one launch for any n and any buffer size (64-bit
 // offsets, per-round buffer resources); the kernel finds its own workgroup ranges.
 int launch_stream(DevState &s, const uint8_t *base, uint64_t nbytes, const uint64_t *offs, const uint32_t *lens,
@@ -2580,7 +1904,6 @@ namespace dev {
 struct FixedProvL {
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
-    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride, lead;
     uint32_t len;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
@@ -2594,7 +1917,6 @@ struct FixedProvL {
 struct ArrayProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
-    static constexpr bool kSmall = WTP_PC_SMALL;  // see k_pieces' small-packet phase
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
@@ -2604,8 +1926,6 @@ struct ArrayProvL {
     }
     __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
     __device__ __forceinline__ const uint32_t *len_array() const { return lens; }
-    __device__ __forceinline__ const uint32_t *off_array() const { return reinterpret_cast<const uint32_t *>(offs); }
-    __device__ __forceinline__ uint32_t view_lead() const { return uint32_t(lead); }
     __device__ __forceinline__ uint32_t len_of(uint32_t w) const { return w; }
     __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
                                            uint32_t &) const {
@@ -2622,7 +1942,6 @@ struct ArrayProvL {
 struct DgramProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
-    static constexpr bool kSmall = false;  // see k_pieces' small-packet phase
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
@@ -2747,17 +2066,10 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     // fast path, any other layout on its lane-per-payload path, exact either way.
     if (((lead + base_bytes + 15) & ~uint64_t(15)) >= (1ull << 31))
         return launch_stream(*s, b, base_bytes, d_offsets, d_lengths, n, d_out, st);
-    // k_pieces; WTP_BRAID_VAR=1 in the environment selects the experimental braided
-    // mixed-length kernel (measured slower on C5)
-    const char *bv = getenv("WTP_BRAID_VAR");
-    const bool use_pieces = !(bv && bv[0] == '1');
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
-        if (use_pieces)
-            rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
-                               dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
-        else
-            rc = launch_braid_var(*s, b, base_bytes, d_offsets + p, d_lengths + p, cnt, dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
+        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
+                           dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
         if (rc) break;
     }
     return rc;

@@ -134,66 +134,6 @@ def pieces_crc(T: Tables, buf: bytes, off: int, L: int) -> int:
     return W[K - 1] ^ T.init_const(L)
 
 
-def braid_var_crc(T: Tables, buf: bytes, off: int, L: int) -> int:
-    """k_braid_var's braided phase for one packet of any byte offset (64 < L <= 1536):
-    an end-aligned frame of R = ceil(L/256) rows (frame bytes before the packet masked
-    to zero in row 0, the only row that can hold them), the braid loop and in-lane fold
-    of k_fixed_braid, the flush without a trailing-zero fix (the frame ends at the
-    packet end), then crc = acc ^ init_const(L) (the kernel's LDS cinit table)."""
-    R = (L + 255) // 256
-    end = off + L
-    fs = end - 256 * R
-    assert 0 <= off - fs < 256
-    frame = bytearray(256 * R)
-    for t in range(256 * R):
-        g = fs + t
-        if g >= off:
-            frame[t] = buf[g]
-    b = [[int.from_bytes(frame[j * 16 + 4 * k:j * 16 + 4 * k + 4], "little") for k in range(4)] for j in range(G)]
-    for i in range(1, R):
-        for j in range(G):
-            c = (i * G + j) * 16
-            for k in range(4):
-                b[j][k] = _apply(T.braid, b[j][k]) ^ int.from_bytes(frame[c + 4 * k:c + 4 * k + 4], "little")
-    v = []
-    for j in range(G):
-        x = _apply(T.inv[4], b[j][3]) ^ b[j][2]
-        x = _apply(T.inv[4], x) ^ b[j][1]
-        v.append(_apply(T.inv[4], x) ^ b[j][0])
-    halves = []
-    for h in (0, 1):
-        acc = v[8 * h + 7]
-        for jj in range(6, -1, -1):
-            acc = _apply(T.inv[16], acc) ^ v[8 * h + jj]
-        if h:
-            acc = _apply(T.inv[128], acc)
-        halves.append(acc)
-    return _apply(T.braid, halves[0] ^ halves[1]) ^ T.init_const(L)
-
-
-def small_crc(T: Tables, buf: bytes, off: int, L: int, W: int) -> int:
-    """k_braid_var's small-packet rounds: one lane per packet (L <= W, W = 16 or 64), the
-    W-byte window ending at the packet end (bytes before the packet masked), words
-    combined backwards by Horner with x^-32 into S = sum_i x^(-32 i) w_i, then
-    R_0 = x^(8 W) S applied as T256 (x^2048) after x^-1024 and (2048 - 8 W - 1024) / 128
-    steps of x^-128, crc = R_0 ^ init_const(L)."""
-    end = off + L
-    win = bytearray(W)
-    for t in range(W):
-        g = end - W + t
-        if g >= off:
-            win[t] = buf[g]
-    n = W // 4
-    w = [int.from_bytes(win[4 * i:4 * i + 4], "little") for i in range(n)]
-    acc = w[n - 1]
-    for i in range(n - 2, -1, -1):
-        acc = _apply(T.inv[4], acc) ^ w[i]
-    for _ in range((2048 - 8 * W - 1024) // 128):
-        acc = _apply(T.inv[16], acc)
-    acc = _apply(T.inv[128], acc)
-    return _apply(T.braid, acc) ^ T.init_const(L)
-
-
 # ---- k_pieces round structure (staging + lane assignment) --------------------------
 PC_CHUNKS = 272
 PC_SLOT = 4640

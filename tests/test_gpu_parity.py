@@ -197,22 +197,9 @@ def _forced_stream(W):
     return call
 
 
-# wtp_crc32_batch_var with WTP_BRAID_VAR=1 (k_braid_var, the experimental braided
-# mixed-length kernel, instead of k_pieces below 2 GiB).
-def _forced_braid_var(W):
-    def call(*a, **k):
-        os.environ["WTP_BRAID_VAR"] = "1"
-        try:
-            return W.crc32_batch_var(*a, **k)
-        finally:
-            del os.environ["WTP_BRAID_VAR"]
-    return call
-
-
-@pytest.fixture(params=["var", "packed", "braid_var", "stream"])
+@pytest.fixture(params=["var", "packed", "stream"])
 def VAR(W, request):
-    return {"var": W.crc32_batch_var, "packed": W.crc32_batch_packed, "braid_var": _forced_braid_var(W),
-            "stream": _forced_stream(W)}[request.param]
+    return {"var": W.crc32_batch_var, "packed": W.crc32_batch_packed, "stream": _forced_stream(W)}[request.param]
 
 
 @pytest.mark.parametrize("n,s", [(200_000, 1.1), (1 << 20, 1.1), (1 << 20, 1.0), (1 << 20, 1.2)])
@@ -292,7 +279,7 @@ def test_var_shuffled_offsets_and_empty(W, VAR):
 # Mixed-length batches: large batches, lengths around the piece boundaries up to the
 # 4096-B limit, unordered/overlapping offsets, empty payloads, an unaligned base.
 @pytest.mark.parametrize("case", ["uniform_shuffled", "all_long_packed", "all_short", "boundary_lengths", "zipf1.0_lead",
-                                  "multi_segment", "braid_rows", "small_runs"])
+                                  "multi_segment", "row_boundaries", "small_runs"])
 def test_var_mixed_cases(W, VAR, case):
     rng = np.random.default_rng(11)
     n = {"uniform_shuffled": 100_000, "multi_segment": 1_300_000}.get(case, 70_000)
@@ -309,13 +296,11 @@ def test_var_mixed_cases(W, VAR, case):
         elif case == "boundary_lengths":  # around chunk-count boundaries, up to the 4096-B limit
             lens = np.array([1, 2, 15, 16, 17, 191, 192, 193, 255, 256, 257, 1505, 1520, 1521, 1536, 1537, 4095,
                              4096], np.uint32)[rng.integers(0, 18, n)]
-        elif case == "braid_rows":  # k_braid_var: every row count, mixed-row rounds, heads whose
-            # injected first 4 bytes reach into row 1 (len % 256 in 1..3), the small/braided
-            # boundary (64/65) and the fix-up above 1536
+        elif case == "row_boundaries":  # lengths around 64 B pieces and 256 B rows, to 2000 B
             lens = np.array([1, 16, 17, 63, 64, 65, 66, 255, 256, 257, 258, 259, 260, 511, 512, 513, 514, 515, 767,
                              769, 1025, 1027, 1281, 1283, 1455, 1456, 1535, 1536, 1537, 2000], np.uint32)[
                 rng.integers(0, 30, n)]
-        elif case == "small_runs":  # long runs of small packets: empty 64-packet groups in phase B
+        elif case == "small_runs":  # long runs of <= 64-B packets with rare long ones
             lens = rng.integers(0, 65, n).astype(np.uint32)
             lens[rng.integers(0, n, n // 500)] = 700
         elif case == "multi_segment":  # > 1 segment per workgroup: the next segment's prefetch

@@ -71,7 +71,6 @@ for s in $STEPS; do
     copyprobe) run copyprobe 120 ./tools/bin/copyprobe ;;
     ualprobe) run ualprobe 120 ./tools/bin/ualprobe ;;
     abbuild) run abbuild 300 python tools/ab_lib.py --what build ${AB_LIBS} ;;
-    abc5env) run abc5env 300 python tools/ab_c5_env.py --out "$OUT/abc5env.json" ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
