@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -267,6 +268,41 @@ static int host_verify_loop(Pipe *P, const uint8_t *h, bool pinned, size_t strid
     return WTP_OK;
 }
 
+// Device address of page-locked host memory (hipHostMalloc / wtp_host_alloc memory is
+// mapped into the device's address space), or null for any other pointer.
+static void *dev_view(const void *h) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, h) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
+// Small batches from a pinned ring and pinned lengths (wReceiver's window-size batches):
+// the kernel reads the ring and the lengths in place over PCIe and writes ok / crc into
+// the pipeline's pinned result buffers, so a call is one launch and one synchronisation
+// instead of four copies around the launch.  Rings up to kZeroCopyBytes (4 MiB); larger ones
+// take the copy pipeline (two slabs in flight), which streams PCIe at the link rate.
+constexpr size_t kZeroCopyBytes = size_t(4) << 20;
+static bool zero_copy_enabled() {
+    const char *e = getenv("WTP_HOST_ZEROCOPY");  // 0 disables (A/B measurements, tests)
+    return !(e && e[0] == '0');
+}
+
+static int host_verify_zero_copy(Pipe *P, const void *dr, size_t stride, const void *dl, size_t n, uint8_t *h_ok,
+                                 uint32_t *h_crc_out) {
+    void *dok = dev_view(P->pin_ok[0]), *dcrc = dev_view(P->pin_out[0]);
+    if (!dok || !dcrc) return hfail(WTP_EHIP, "pipeline result buffers are not device-mapped", hipSuccess);
+    int rc = wtp_crc32_verify_batch(dr, stride, static_cast<const uint32_t *>(dl), n, static_cast<uint8_t *>(dok),
+                                    static_cast<uint32_t *>(dcrc), P->st[0]);
+    if (rc) return rc;
+    H_HIP(hipStreamSynchronize(P->st[0]));
+    memcpy(h_ok, P->pin_ok[0], n);
+    if (h_crc_out) memcpy(h_crc_out, P->pin_out[0], n * 4);
+    return WTP_OK;
+}
+
 int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len, size_t n, uint8_t *h_ok,
                           uint32_t *h_crc_out) {
     if (n == 0) return WTP_OK;
@@ -276,9 +312,14 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     int rc = pipe_get(P);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(P->mu);
-    // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
-    rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), is_pinned(h_dgrams), stride, h_recv_len,
-                          is_pinned(h_recv_len), n, h_ok, h_crc_out);
+    const void *dr = dev_view(h_dgrams), *dl = dev_view(h_recv_len);
+    if (dr && dl && n <= P->max_pk && n * stride <= kZeroCopyBytes && zero_copy_enabled()) {
+        rc = host_verify_zero_copy(P, dr, stride, dl, n, h_ok, h_crc_out);
+    } else {
+        // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
+        rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), dr != nullptr, stride, h_recv_len,
+                              dl != nullptr, n, h_ok, h_crc_out);
+    }
     if (rc) drain(P);
     return rc;
 }

@@ -942,6 +942,31 @@ def test_host_verify_pinned_ring(W):
     lens.free()
 
 
+@pytest.mark.parametrize("zero_copy", ["1", "0"])
+@pytest.mark.parametrize("n,stride,skip", [(10, 1504, 0), (64, 1472, 3), (700, 1472, 17), (2800, 1472, 1), (300, 1500, 5)])
+def test_host_verify_pinned_small_batches(W, zero_copy, n, stride, skip):
+    """Window-size batches from a pinned ring: rings up to 1 MiB are read by the kernel in
+    place (zero copy, WTP_HOST_ZEROCOPY unset) or through the copy pipeline (=0); the
+    ring and the lengths start `skip` slots into their pinned allocations (wReceiver hands
+    the library a batch inside its ring); a 1500-B stride takes the general kernel."""
+    rng = np.random.default_rng(n + stride)
+    buf, rl = _full_ring(n, stride, rng, 0.85)
+    ring = W.PinnedBuffer((n + skip) * stride)
+    ring.array[skip * stride:] = buf
+    lens = W.PinnedBuffer((n + skip) * 4)
+    la = lens.array.view(np.uint32)
+    la[skip:] = rl
+    os.environ["WTP_HOST_ZEROCOPY"] = zero_copy
+    try:
+        ok, crc = W.host_verify(ring.array[skip * stride:], stride, la[skip:])
+    finally:
+        del os.environ["WTP_HOST_ZEROCOPY"]
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    assert np.array_equal(ok, want_ok) and np.array_equal(crc, want_crc)
+    ring.free()
+    lens.free()
+
+
 def test_build_data_packets(W):
     for total in (64, 1456, 2216, 10202, 1456 * 300 + 17):
         host = O.synth_fill_np(total, start_byte=total)

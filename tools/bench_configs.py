@@ -298,7 +298,7 @@ def hostverify():
     pageable = np.empty(nmax * stride, np.uint8)
     pageable[:] = ring.array
     plens = la.copy()
-    for n in (10, 64, 1024, 16384, nmax):
+    for n in (10, 64, 1024, 2560, 16384, nmax):
         for kind, bp, lp in (("pinned", ring.ptr, lens.ptr), ("pageable", pageable.ctypes.data, plens.ctypes.data)):
             # last datagram of the batch short: the fix-up phase runs, as with a file's tail
             save_p, save_l = la[n - 1], plens[n - 1]
