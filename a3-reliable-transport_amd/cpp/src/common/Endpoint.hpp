@@ -140,13 +140,15 @@ class RecvRing {
    public:
     static constexpr size_t kRecv = 1500;  // Receiver.cpp:123 char buffer[1500]
     static constexpr size_t kSlot = 1504;  // kRecv rounded up to 16
-    // pinned: allocate the ring with wtp_host_alloc (GPU verify: one DMA per batch);
-    // otherwise plain page-aligned memory (CPU verify needs no device).
+    // pinned: allocate the ring and its recv_len array with wtp_host_alloc (GPU verify:
+    // batches up to 4 MiB are read by the kernel in place, larger ones take one DMA per
+    // slab); otherwise plain page-aligned memory (CPU verify needs no device).
     RecvRing(size_t slots, bool pinned)
         : n_(slots), pinned_(pinned),
           buf_(static_cast<uint8_t *>(pinned ? wtp_host_alloc(slots * kSlot) : std::aligned_alloc(4096, round4k(slots * kSlot)))),
-          len_(slots), ok_(slots), iov_(slots), msg_(slots), peer_(slots) {
-        if (!buf_) throw std::runtime_error("receive ring allocation failed");
+          len_(static_cast<uint32_t *>(pinned ? wtp_host_alloc(slots * 4) : std::aligned_alloc(4096, round4k(slots * 4)))),
+          ok_(slots), iov_(slots), msg_(slots), peer_(slots) {
+        if (!buf_ || !len_) throw std::runtime_error("receive ring allocation failed");
         for (size_t i = 0; i < n_; ++i) {
             iov_[i] = {buf_ + i * kSlot, kRecv};
             msg_[i].msg_hdr.msg_iov = &iov_[i];
@@ -154,10 +156,13 @@ class RecvRing {
         }
     }
     ~RecvRing() {
-        if (pinned_)
+        if (pinned_) {
             wtp_host_free(buf_);
-        else
+            wtp_host_free(len_);
+        } else {
             std::free(buf_);
+            std::free(len_);
+        }
     }
     RecvRing(const RecvRing &) = delete;
     RecvRing &operator=(const RecvRing &) = delete;
@@ -177,7 +182,7 @@ class RecvRing {
     }
     uint8_t *slot(size_t i) { return buf_ + i * kSlot; }
     uint32_t len(size_t i) const { return len_[i]; }
-    const uint32_t *lens() const { return len_.data(); }
+    const uint32_t *lens() const { return len_; }
     uint8_t *ok() { return ok_.data(); }
     const sockaddr_in &peer(size_t i) const { return peer_[i]; }
     uint8_t *ring() { return buf_; }
@@ -187,7 +192,7 @@ class RecvRing {
     size_t n_;
     bool pinned_;
     uint8_t *buf_;
-    std::vector<uint32_t> len_;
+    uint32_t *len_;  // recv_len per slot (pinned with the ring)
     std::vector<uint8_t> ok_;
     std::vector<iovec> iov_;
     std::vector<mmsghdr> msg_;
