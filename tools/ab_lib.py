@@ -22,6 +22,7 @@ from bench import TimingEvent  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--what", default="build")
 ap.add_argument("--rounds", type=int, default=15)
+ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("libs", nargs="+")
 a = ap.parse_args()
 
@@ -40,7 +41,7 @@ for p in a.libs:
 L0 = libs[0]
 st = torch.cuda.current_stream()
 sp = st.cuda_stream
-n = 1 << 20
+n = a.n
 P = 1456
 if a.what in ("build", "crc", "verify"):
     pay = torch.empty(n * P + 64, dtype=torch.uint8, device="cuda")
