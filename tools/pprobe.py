@@ -49,5 +49,10 @@ dur = (s[:, :, 5][live] - s[:, :, 3][live]) / 100.0
 print(f"  rounds/wave min {r.min()} mean {r.mean():.1f} max {r.max()}; loop us mean {dur.mean():.2f} max {dur.max():.2f};"
       f" us/round mean {np.mean(dur / np.maximum(r, 1)):.2f}")
 print(f"  packets/wave min {s[:, :, 7][live].min()} max {s[:, :, 7][live].max()}")
+# workgroup ends (last wave of each workgroup): the launch waits for the slowest
+ends = np.where(live, (s[:, :, 5] - t0) / 100.0, -1.0).max(axis=1)
+ends = ends[ends >= 0]
+print(f"  workgroup end min {ends.min():.2f} mean {ends.mean():.2f} p90 {np.percentile(ends, 90):.2f} "
+      f"max {ends.max():.2f} us (perfect cross-workgroup balance would end near the mean)")
 if os.environ.get("PPROBE_DUMP"):
     np.save(os.environ["PPROBE_DUMP"], s)
