@@ -290,10 +290,8 @@ static bool zero_copy_enabled() {
     return !(e && e[0] == '0');
 }
 
-static int host_verify_zero_copy(Pipe *P, const void *dr, size_t stride, const void *dl, size_t n, uint8_t *h_ok,
-                                 uint32_t *h_crc_out) {
-    void *dok = dev_view(P->pin_ok[0]), *dcrc = dev_view(P->pin_out[0]);
-    if (!dok || !dcrc) return hfail(WTP_EHIP, "pipeline result buffers are not device-mapped", hipSuccess);
+static int host_verify_zero_copy(Pipe *P, const void *dr, size_t stride, const void *dl, size_t n, void *dok,
+                                 void *dcrc, uint8_t *h_ok, uint32_t *h_crc_out) {
     int rc = wtp_crc32_verify_batch(dr, stride, static_cast<const uint32_t *>(dl), n, static_cast<uint8_t *>(dok),
                                     static_cast<uint32_t *>(dcrc), P->st[0]);
     if (rc) return rc;
@@ -313,8 +311,13 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     if (rc) return rc;
     std::lock_guard<std::mutex> g(P->mu);
     const void *dr = dev_view(h_dgrams), *dl = dev_view(h_recv_len);
+    void *dok = nullptr, *dcrc = nullptr;  // the pipeline's pinned result buffers, device view
     if (dr && dl && n <= P->max_pk && n * stride <= kZeroCopyBytes && zero_copy_enabled()) {
-        rc = host_verify_zero_copy(P, dr, stride, dl, n, h_ok, h_crc_out);
+        dok = dev_view(P->pin_ok[0]);
+        dcrc = dev_view(P->pin_out[0]);
+    }
+    if (dok && dcrc) {
+        rc = host_verify_zero_copy(P, dr, stride, dl, n, dok, dcrc, h_ok, h_crc_out);
     } else {
         // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
         rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), dr != nullptr, stride, h_recv_len,

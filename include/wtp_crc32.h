@@ -166,7 +166,11 @@ int wtp_crc32_host_chunked(const void *h_buf, size_t nbytes, size_t chunk, uint3
 int wtp_crc32_host_chunked_multi(const void *h_buf, size_t nbytes, size_t chunk, uint32_t *h_out,
                                  const int *devices, int ndev);
 
-/* The wReceiver path, host buffers: same semantics as wtp_crc32_verify_batch. */
+/* The wReceiver path, host buffers: same semantics as wtp_crc32_verify_batch.  When the
+   ring and recv_len both live in page-locked memory (wtp_host_alloc) and the ring is at
+   most 4 MiB, the kernel reads them in place (one launch + one sync per call); other
+   batches go through the library's pinned double-buffered copy pipeline.
+   WTP_HOST_ZEROCOPY=0 in the environment forces the pipeline. */
 int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len,
                           size_t n, uint8_t *h_ok, uint32_t *h_crc_out);
 
