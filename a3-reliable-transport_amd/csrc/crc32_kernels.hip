@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict
 // LDS after the braided rounds (the piece layout for 8 waves): tables [0, kPcStage),
 // staging slots of waves 0..7, the index list where slots 8..15 of k_pieces would be,
 // flags at kPcFlags, control words (per-wave counts, list length) past kPcLdsWords.
-constexpr uint32_t kVfWaves = 8;  // the verify launch's 512 threads (kBraidThreads)
+constexpr uint32_t kVfWaves = 8;  // the verify launch's 512 threads (VerifyBEpi::kThreads)
 constexpr uint32_t kVfList = kPcStage + kVfWaves * kPcSlot;
 constexpr uint32_t kVfCap = (kPcFlags - kVfList) / 4;
 constexpr uint32_t kVfCtl = (kPcLdsWords * 4 + 15) & ~15u;
@@ -1819,8 +1819,9 @@ int launch_check(const char *what) {
 // Fewer waves per CU keep fewer rows in flight; HBM serves the stream with less
 // queueing (and, for the builder, fewer read/write turnarounds) while 8 resp. 2 waves,
 // two rounds each, still cover its latency.
-constexpr unsigned kBraidThreads = dev::CrcBEpi::kThreads;
+// (the sizes are each epilogue's kThreads: CrcBEpi and VerifyBEpi 512, BuildBEpi 128)
 static_assert(dev::VerifyBEpi::kThreads == dev::CrcBEpi::kThreads, "one braided grid rule");
+static_assert(dev::VerifyBEpi::kThreads == 64 * dev::kVfWaves, "verify fix-up LDS layout");
 
 template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
