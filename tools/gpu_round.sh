@@ -70,6 +70,7 @@ for s in $STEPS; do
     footprint) run footprint 300 python tools/footprint_probe.py ;;
     copyprobe) run copyprobe 120 ./tools/bin/copyprobe ;;
     ualprobe) run ualprobe 120 ./tools/bin/ualprobe ;;
+    winprobe) run winprobe 120 ./tools/bin/winprobe ;;
     abbuild) run abbuild 300 python tools/ab_lib.py --what build ${AB_LIBS} ;;
     abcrc) run abcrc 300 python tools/ab_lib.py --what crc --n ${AB_N:-1048576} ${AB_LIBS} ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
