@@ -8,10 +8,12 @@
 // advance, END with the START seqNum until ACKed.
 //
 // The checksum path is the one this repository accelerates: the whole file is read up
-// front (as Sender.cpp:82 does; into pinned memory with --crc gpu) and every chunk's CRC
-// is computed in ONE batch — on the MI355X through wtp_crc32_host_chunked with --crc gpu
-// (wtp_crc32_host_chunked_multi over N devices with --gpus N, 0 = all), or with the
-// reference's per-packet crc32() with --crc cpu.  Retransmissions reuse the stored header.
+// front (as Sender.cpp:82 does; into pinned memory with --crc gpu).  With --crc gpu on one
+// device every DATA datagram — header and CRC included (Sender.cpp:187-197) — is built in
+// ONE fused pass by wtp_host_build_data_packets into a pinned wire buffer, and sending is
+// a pointer into it.  With --gpus N (0 = all) every chunk's CRC is computed in one batch by
+// wtp_crc32_host_chunked_multi, and with --crc cpu by the reference's per-packet crc32();
+// those two paths write the header per send.  Retransmissions resend the same bytes.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +21,7 @@
 #include <fstream>
 #include <iostream>
 #include <iterator>
+#include <memory>
 #include <random>
 #include <vector>
 
@@ -84,6 +87,31 @@ class InputFile {
     size_t n_ = 0;
 };
 
+// Every DATA datagram of the file in one pinned buffer, slot i = [i*kSlot, +len(i)),
+// built on the device by the fused builder (--crc gpu on one device).
+class WireBuffer {
+   public:
+    static constexpr size_t kSlot = kHeaderBytes + kMaxPayload;  // 1472 = 92 * 16: the braided path
+    explicit WireBuffer(const InputFile &file) : n_((file.size() + kMaxPayload - 1) / kMaxPayload) {
+        if (!n_) return;
+        p_ = static_cast<uint8_t *>(wtp_host_alloc(n_ * kSlot));
+        if (!p_) throw std::runtime_error("cannot pin the wire buffer");
+        if (wtp_host_build_data_packets(file.data(), file.size(), 0, p_, kSlot, nullptr) != WTP_OK) {
+            wtp_host_free(p_);
+            throw std::runtime_error(std::string("wtp_host_build_data_packets: ") + wtp_last_error());
+        }
+    }
+    ~WireBuffer() { wtp_host_free(p_); }
+    WireBuffer(const WireBuffer &) = delete;
+    WireBuffer &operator=(const WireBuffer &) = delete;
+    const uint8_t *slot(uint32_t i) const { return p_ + size_t(i) * kSlot; }
+    size_t count() const { return n_; }
+
+   private:
+    size_t n_;
+    uint8_t *p_ = nullptr;
+};
+
 struct Conn {
     int fd;
     sockaddr_in peer;
@@ -141,9 +169,16 @@ int main(int argc, char **argv) {
         // pinned memory, so the CRC pipeline DMAs it to the device without staging.
         const InputFile file(a.get("input"), crc.gpu());
 
-        // Every DATA checksum in one batch (the device path when --crc gpu).
-        const std::vector<uint32_t> sums = crc.chunks(file.data(), file.size());
-        const uint32_t nchunks = uint32_t(sums.size());
+        // Every DATA datagram built on the device (--crc gpu, one device), else every DATA
+        // checksum in one batch (the device path when --crc gpu --gpus N).
+        const bool fused = crc.gpu() && std::stoi(a.get("gpus", "1")) == 1;
+        std::unique_ptr<WireBuffer> built;
+        std::vector<uint32_t> sums;
+        if (fused)
+            built = std::make_unique<WireBuffer>(file);
+        else
+            sums = crc.chunks(file.data(), file.size());
+        const uint32_t nchunks = uint32_t(fused ? built->count() : sums.size());
 
         Conn c{udp_socket(), addr_of(a.get("host"), port), log};
         set_rcv_timeout_ms(c.fd, 50);
@@ -156,7 +191,10 @@ int main(int argc, char **argv) {
         auto send_chunk = [&](uint32_t i) {
             const size_t off = size_t(i) * kMaxPayload;
             const uint32_t len = uint32_t(std::min(kMaxPayload, file.size() - off));
-            c.send(wire, make_datagram(wire, DATA, i, file.data() + off, len, sums[i]));
+            if (fused)
+                c.send(built->slot(i), kHeaderBytes + len);
+            else
+                c.send(wire, make_datagram(wire, DATA, i, file.data() + off, len, sums[i]));
         };
 
         uint32_t base = 0, next = 0;  // window = [base, next)

@@ -61,6 +61,10 @@ struct Pipe {
     uint8_t *pin_ok[2] = {nullptr, nullptr};
     uint8_t *dev_ok[2] = {nullptr, nullptr};
     size_t max_pk = 0;                           // packets per slab (results capacity)
+    std::once_flag wire_once;                    // the builder's wire slabs, made on first use
+    int wire_rc = WTP_OK;
+    uint8_t *dev_wire[2] = {nullptr, nullptr};
+    uint8_t *pin_wire[2] = {nullptr, nullptr};
 };
 Pipe g_pipe[64];
 
@@ -279,14 +283,78 @@ static void *dev_view(const void *h) {
     return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
 }
 
+// Host wrapper of the fused DATA builder (wSender --crc gpu; SURVEY.md §8f row 1,
+// Packet.cpp:9-14,40-47, Sender.cpp:187-197): slabs of whole 1456-B chunks go H2D
+// (pinned sources directly, pageable ones through the staging copy), wtp_build_data_packets
+// writes their datagrams into a device wire slab, which comes back D2H straight into a
+// pinned h_wire (else through a pinned slab); two slabs in flight.
+static int wire_slabs(Pipe *P) {
+    std::call_once(P->wire_once, [P] {
+        auto mk = [P]() -> int {
+            for (int b = 0; b < 2; ++b) {
+                H_HIP(hipMalloc(reinterpret_cast<void **>(&P->dev_wire[b]), kSlabBytes));
+                H_HIP(hipHostMalloc(reinterpret_cast<void **>(&P->pin_wire[b]), kSlabBytes, hipHostMallocDefault));
+            }
+            return WTP_OK;
+        };
+        P->wire_rc = mk();
+    });
+    return P->wire_rc ? hfail(P->wire_rc, "builder wire slabs", hipSuccess) : WTP_OK;
+}
+
+static int host_build_loop(Pipe *P, const uint8_t *h, size_t total, uint32_t seq0, uint8_t *h_wire, size_t ws,
+                           uint32_t *h_wire_len) {
+    constexpr size_t kChunk = 1456;
+    const size_t n = (total + kChunk - 1) / kChunk;
+    const bool pin_src = dev_view(h) != nullptr, pin_wire = dev_view(h_wire) != nullptr;
+    const bool pin_len = h_wire_len && dev_view(h_wire_len) != nullptr;
+    const size_t per = std::min({P->max_pk, kSlabBytes / kChunk, kSlabBytes / ws});
+    struct {
+        size_t first = 0, count = 0;
+        bool live = false;
+    } slot[2];
+    for (size_t first = 0, s = 0; first < n || slot[0].live || slot[1].live; ++s) {
+        const int b = int(s & 1);
+        auto &sl = slot[b];
+        if (sl.live) {
+            H_HIP(hipStreamSynchronize(P->st[b]));
+            if (!pin_wire) memcpy(h_wire + sl.first * ws, P->pin_wire[b], sl.count * ws);
+            if (h_wire_len && !pin_len) memcpy(h_wire_len + sl.first, P->pin_aux[b], sl.count * 4);
+            sl.live = false;
+        }
+        if (first >= n) continue;
+        const size_t cnt = std::min(per, n - first);
+        const size_t bytes = first + cnt == n ? total - first * kChunk : cnt * kChunk;
+        const uint8_t *src = h + first * kChunk;
+        if (!pin_src) {
+            stage_copy(P->pin_in[b], src, bytes);
+            src = P->pin_in[b];
+        }
+        H_HIP(hipMemcpyAsync(P->dev_in[b], src, bytes, hipMemcpyHostToDevice, P->st[b]));
+        int rc = wtp_build_data_packets(P->dev_in[b], bytes, seq0 + uint32_t(first), P->dev_wire[b], ws,
+                                        h_wire_len ? P->dev_aux[b] : nullptr, P->st[b]);
+        if (rc) return rc;
+        H_HIP(hipMemcpyAsync(pin_wire ? h_wire + first * ws : P->pin_wire[b], P->dev_wire[b], cnt * ws,
+                             hipMemcpyDeviceToHost, P->st[b]));
+        if (h_wire_len)
+            H_HIP(hipMemcpyAsync(pin_len ? h_wire_len + first : P->pin_aux[b], P->dev_aux[b], cnt * 4,
+                                 hipMemcpyDeviceToHost, P->st[b]));
+        sl.first = first;
+        sl.count = cnt;
+        sl.live = true;
+        first += cnt;
+    }
+    return WTP_OK;
+}
+
 // Small batches from a pinned ring and pinned lengths (wReceiver's window-size batches):
 // the kernel reads the ring and the lengths in place over PCIe and writes ok / crc into
 // the pipeline's pinned result buffers, so a call is one launch and one synchronisation
 // instead of four copies around the launch.  Rings up to kZeroCopyBytes (4 MiB); larger ones
 // take the copy pipeline (two slabs in flight), which streams PCIe at the link rate.
 constexpr size_t kZeroCopyBytes = size_t(4) << 20;
-static bool zero_copy_enabled() {
-    const char *e = getenv("WTP_HOST_ZEROCOPY");  // 0 disables (A/B measurements, tests)
+static bool zero_copy_enabled(const char *var = "WTP_HOST_ZEROCOPY") {
+    const char *e = getenv(var);  // 0 disables (A/B measurements, tests)
     return !(e && e[0] == '0');
 }
 
@@ -323,6 +391,35 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
         rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), dr != nullptr, stride, h_recv_len,
                               dl != nullptr, n, h_ok, h_crc_out);
     }
+    if (rc) drain(P);
+    return rc;
+}
+
+int wtp_host_build_data_packets(const void *h_payloads, size_t total_bytes, uint32_t seq0, void *h_wire,
+                                size_t wire_stride, uint32_t *h_wire_len) {
+    if (total_bytes == 0) return WTP_OK;
+    if (!h_payloads || !h_wire) return hfail(WTP_EINVAL, "null pointer", hipSuccess);
+    if (wire_stride < 16 + 1456 || wire_stride > kSlabBytes) return hfail(WTP_EINVAL, "bad wire stride", hipSuccess);
+    Pipe *P = nullptr;
+    int rc = pipe_get(P);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(P->mu);
+    const void *ds = dev_view(h_payloads);
+    void *dw = dev_view(h_wire), *dln = h_wire_len ? dev_view(h_wire_len) : nullptr;
+    if (ds && dw && (!h_wire_len || dln) && zero_copy_enabled("WTP_HOST_BUILD_ZEROCOPY")) {
+        // pinned both ways: the builder reads the payloads and writes the datagrams across
+        // the link itself, both directions at once, no device staging
+        rc = wtp_build_data_packets(ds, total_bytes, seq0, dw, wire_stride, static_cast<uint32_t *>(dln), P->st[0]);
+        if (!rc) {
+            hipError_t e = hipStreamSynchronize(P->st[0]);
+            if (e != hipSuccess) rc = hfail(WTP_EHIP, "builder zero copy", e);
+        }
+        if (rc) drain(P);
+        return rc;
+    }
+    if ((rc = wire_slabs(P))) return rc;
+    rc = host_build_loop(P, static_cast<const uint8_t *>(h_payloads), total_bytes, seq0, static_cast<uint8_t *>(h_wire),
+                         wire_stride, h_wire_len);
     if (rc) drain(P);
     return rc;
 }

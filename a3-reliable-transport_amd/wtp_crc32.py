@@ -50,6 +50,7 @@ def _load() -> C.CDLL:
         "wtp_crc32_host_chunked": (i32, [vp, sz, sz, vp]),
         "wtp_crc32_host_chunked_multi": (i32, [vp, sz, sz, vp, vp, i32]),
         "wtp_crc32_host_verify": (i32, [vp, sz, vp, sz, vp, vp]),
+        "wtp_host_build_data_packets": (i32, [vp, sz, u32, vp, sz, vp]),
         "wtp_host_alloc": (vp, [sz]),
         "wtp_host_free": (None, [vp]),
         "wtp_synth_fill": (i32, [vp, u64, sz, u64, vp]),
@@ -64,8 +65,8 @@ def _load() -> C.CDLL:
 LIB = _load()
 EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_reserve_cus", "wtp_crc32",
             "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_batch_packed", "wtp_crc32_verify_batch", "wtp_build_data_packets",
-            "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify", "wtp_host_alloc",
-            "wtp_host_free", "wtp_synth_fill")
+            "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify",
+            "wtp_host_build_data_packets", "wtp_host_alloc", "wtp_host_free", "wtp_synth_fill")
 
 
 def _check(rc: int, what: str) -> None:
@@ -183,6 +184,24 @@ def host_verify(dgrams: np.ndarray, stride: int, recv_len: np.ndarray):
     _check(LIB.wtp_crc32_host_verify(_np_ptr(dgrams), stride, _np_ptr(recv_len), n, _np_ptr(ok), _np_ptr(crc)),
            "host_verify")
     return ok, crc
+
+
+def host_build_data_packets(payloads: np.ndarray, seq0: int = 0, wire_stride: int = 16 + MAX_PAYLOAD, wire=None,
+                            wire_len=None, nbytes: int | None = None):
+    """Every DATA datagram of a host buffer (wtp_host_build_data_packets); wire / wire_len
+    may be given (e.g. PinnedBuffer arrays), else numpy arrays are allocated.  Slot bytes
+    past each datagram are unspecified."""
+    nb = payloads.nbytes if nbytes is None else nbytes
+    n = (nb + MAX_PAYLOAD - 1) // MAX_PAYLOAD
+    if wire is None:
+        wire = np.zeros(n * wire_stride, dtype=np.uint8)
+    if wire_len is None:
+        wire_len = np.zeros(n, dtype=np.uint32)
+    if wire.nbytes < n * wire_stride or wire_len.nbytes < n * 4:
+        raise WtpError("wire buffers too small")
+    _check(LIB.wtp_host_build_data_packets(_np_ptr(payloads), nb, seq0, _np_ptr(wire), wire_stride,
+                                           _np_ptr(wire_len)), "host_build_data_packets")
+    return wire, wire_len
 
 
 class PinnedBuffer:

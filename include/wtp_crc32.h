@@ -174,6 +174,13 @@ int wtp_crc32_host_chunked_multi(const void *h_buf, size_t nbytes, size_t chunk,
 int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h_recv_len,
                           size_t n, uint8_t *h_ok, uint32_t *h_crc_out);
 
+/* The fused builder from and to host memory (wSender --crc gpu): same layout as
+   wtp_build_data_packets; the bytes of a wire slot past its datagram are unspecified.
+   Pinned (wtp_host_alloc) payloads and wire buffers move by DMA directly, others through
+   the library's pinned slabs; synchronous. */
+int wtp_host_build_data_packets(const void *h_payloads, size_t total_bytes, uint32_t seq0,
+                                void *h_wire, size_t wire_stride, uint32_t *h_wire_len);
+
 /* Pinned (page-locked) host allocation for zero-copy staging, e.g. wSender reads its
    input file straight into such a buffer.  NULL on failure. */
 void *wtp_host_alloc(size_t bytes);

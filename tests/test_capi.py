@@ -153,6 +153,10 @@ def test_argument_validation_without_device():
     assert L.wtp_crc32_batch_fixed(C.addressof(out), 1456, 5000, 4, C.addressof(out), None) == -1
     assert L.wtp_crc32_verify_batch(C.addressof(out), 8, C.addressof(out), 1, C.addressof(out), None, None) == -1
     assert L.wtp_crc32_host_chunked(C.addressof(out), 10, 0, C.addressof(out)) == -1
+    # host builder: nothing to build, null buffers, a wire slot shorter than a full datagram
+    assert L.wtp_host_build_data_packets(None, 0, 0, None, 1472, None) == 0
+    assert L.wtp_host_build_data_packets(None, 10, 0, C.addressof(out), 1472, None) == -1
+    assert L.wtp_host_build_data_packets(C.addressof(out), 4, 0, C.addressof(out), 1471, None) == -1
 
 
 def test_version_string():

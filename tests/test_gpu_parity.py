@@ -1023,6 +1023,66 @@ def test_build_data_packets_paths(W, total, stride, pay_off, wire_off, with_len,
     assert np.array_equal(hdr.copy().view(">u4").ravel(), c)
 
 
+@pytest.mark.parametrize("total,stride,pin_src,pin_wire,with_len,seq0", [
+    (1456 * 50000 + 333, 1472, False, False, True, 5),   # two slabs, pageable both ways, short tail
+    (1456 * 50000 + 333, 1472, True, True, True, 5),     # two slabs, pinned both ways (DMA in place)
+    (1456 * 1000, 1488, True, False, False, 0xFFFFFFF0),  # wider slots, no lengths, seq wraps
+    (1456 * 10 + 1, 1500, False, True, True, 1),         # stride % 16 != 0: the three-step path
+    (100, 1472, True, True, True, 0),                    # one short datagram
+])
+@pytest.mark.parametrize("zero_copy", ["1", "0"])
+def test_host_build_data_packets(W, total, stride, pin_src, pin_wire, with_len, seq0, zero_copy):
+    """wtp_host_build_data_packets (wSender --crc gpu) against the device builder on the same
+    payloads (itself checked against the oracle above) and the oracle on sampled chunks.
+    Pinned both ways the builder works on host memory in place unless
+    WTP_HOST_BUILD_ZEROCOPY=0, which sends it through the device slabs."""
+    if zero_copy == "0" and not (pin_src and pin_wire):
+        pytest.skip("the zero-copy switch only matters when both buffers are pinned")
+    host = O.synth_fill_np(total, start_byte=total ^ stride)
+    nch = (total + 1455) // 1456
+    bufs = []
+    if pin_src:
+        pb = W.PinnedBuffer(total)
+        pb.array[:] = host
+        src = pb.array
+        bufs.append(pb)
+    else:
+        src = host
+    wire = wl = None
+    if pin_wire:
+        pw = W.PinnedBuffer(nch * stride)
+        pl = W.PinnedBuffer(nch * 4)
+        wire, wl = pw.array, pl.array.view(np.uint32)
+        bufs += [pw, pl]
+    if not with_len:
+        wl = None
+    os.environ["WTP_HOST_BUILD_ZEROCOPY"] = zero_copy
+    try:
+        got, got_len = W.host_build_data_packets(src, seq0, stride, wire=wire, wire_len=wl) if with_len else (
+            W.host_build_data_packets(src, seq0, stride, wire=wire)[0], None)
+    finally:
+        del os.environ["WTP_HOST_BUILD_ZEROCOPY"]
+    got = got[:nch * stride].reshape(nch, stride)
+    d = dev_u8(host)
+    dw = torch.zeros(nch * stride, dtype=torch.uint8, device="cuda")
+    dl = u32_out(nch)
+    W.build_data_packets(d, total, seq0, dw, stride, dl)
+    torch.cuda.synchronize()
+    want = dw.cpu().numpy().reshape(nch, stride)
+    want_len = to_u32(dl, nch)
+    last = int(want_len[-1])
+    assert np.array_equal(got[:-1, :1472], want[:-1, :1472])
+    assert np.array_equal(got[-1, :last], want[-1, :last])
+    if with_len:
+        assert np.array_equal(np.asarray(got_len[:nch]), want_len)
+    for i in sorted({0, min(1, nch - 1), nch // 2, nch - 1}):
+        p = host[i * 1456:(i + 1) * 1456].tobytes()
+        dg = O.build_datagram((seq0 + i) & 0xFFFFFFFF, p)
+        assert got[i, :len(dg)].tobytes() == dg, i
+    for b in bufs:
+        b.free()
+
+
 def test_host_chunked_pageable_and_pinned(W):
     nbytes = 40 * (1 << 20) + 64  # crosses slab boundaries? (64 MiB slabs) keep moderate
     host = O.synth_fill_np(nbytes, start_byte=5)

@@ -176,13 +176,25 @@ def test_c1_loopback_gpu_crc(binaries, golden, tmp_path):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    for name in ("input.txt", "input3.txt"):
+    # the sender builds every DATA datagram with the fused device builder
+    # (wtp_host_build_data_packets); the receiver verifies on the device
+    for name in ("input.txt", "input2.txt", "input3.txt"):
         src = os.path.join(GOLD, name)
         d = tmp_path / name
         d.mkdir()
         out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu")
         assert open(out, "rb").read() == open(src, "rb").read()
         assert [f"0x{c:08X}" for c in data_log_checksums(slog)] == golden["files"][name]["crc"]
+        assert [f"0x{c:08X}" for c in data_log_checksums(rlog)] == golden["files"][name]["crc"]
+    import oracle as O
+    d = tmp_path / "exact"
+    d.mkdir()
+    src = str(d / "exact.bin")
+    data = O.synth_fill_np(1456 * 7, start_byte=77).tobytes()  # whole chunks only: no short tail
+    open(src, "wb").write(data)
+    out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu")
+    assert open(out, "rb").read() == data
+    assert data_log_checksums(slog) == [O.crc32(data[i * 1456:(i + 1) * 1456]) for i in range(7)]
 
 
 @pytest.mark.gpu

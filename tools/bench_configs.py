@@ -164,6 +164,42 @@ def c3():
     return res
 
 
+def hostbuild():
+    """wSender --crc gpu: a 1 GiB host file -> every DATA datagram (header + CRC + payload)
+    in a host wire buffer through wtp_host_build_data_packets (H2D -> fused builder -> D2H)."""
+    nbytes = 1 << 30
+    n = (nbytes + 1455) // 1456
+    res = {"config": "host builder: 1 GiB host file -> 1472-B DATA datagrams in host memory", "bytes": nbytes,
+           "datagrams": n}
+    pb = W.PinnedBuffer(nbytes)
+    host = pb.array
+    step = 64 << 20
+    for o in range(0, nbytes, step):
+        host[o:o + step] = O.synth_fill_np(min(step, nbytes - o), start_byte=o)
+    pw = W.PinnedBuffer(n * 1472)
+    for label in ("pinned", "pinned_staged", "pageable"):
+        # pinned: the builder reads/writes host memory across the link (zero copy);
+        # pinned_staged: the same buffers through the device slabs (WTP_HOST_BUILD_ZEROCOPY=0)
+        os.environ["WTP_HOST_BUILD_ZEROCOPY"] = "0" if label == "pinned_staged" else "1"
+        src, wire = (host, pw.array) if label != "pageable" else (np.array(host), np.empty(n * 1472, np.uint8))
+        W.host_build_data_packets(src, 0, 1472, wire=wire)  # warm (allocates the wire slabs)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            W.host_build_data_packets(src, 0, 1472, wire=wire)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        ok = all(wire[i * 1472:i * 1472 + 16 + min(1456, nbytes - i * 1456)].tobytes() ==
+                 O.build_datagram(i, host[i * 1456:(i + 1) * 1456].tobytes()) for i in (0, n // 2, n - 1))
+        res[label] = {"seconds": round(t, 4), "payload_GBps": round(nbytes / t / GB, 2),
+                      "moved_GBps": round((nbytes + n * 1472) / t / GB, 2), "parity_spot": ok}
+        del src, wire
+    del os.environ["WTP_HOST_BUILD_ZEROCOPY"]
+    pw.free()
+    pb.free()
+    return res
+
+
 def c5(s, entry="var"):
     """entry "var": wtp_crc32_batch_var (k_pieces, any offsets); "packed":
     wtp_crc32_batch_packed (the C5 layout, payloads back to back: the same k_pieces route
@@ -334,7 +370,7 @@ def hostverify():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="configs.json")
-    ap.add_argument("--only", default="c2,c3,c5,verify,hostverify")
+    ap.add_argument("--only", default="c2,c3,c5,verify,hostverify,hostbuild")
     a = ap.parse_args()
     assert W.LIB.wtp_init(0) == 0
     res = {"device": torch.cuda.get_device_name(0), "host_cpus": os.cpu_count(), "results": []}
@@ -357,6 +393,8 @@ def main():
         add(c3())
     if "hostverify" in sel:
         add(hostverify())
+    if "hostbuild" in sel:
+        add(hostbuild())
 
 
 if __name__ == "__main__":

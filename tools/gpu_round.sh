@@ -33,6 +33,7 @@ nproc > "$OUT/host_cpus.txt"; lscpu 2>/dev/null | grep -m1 "Model name" >> "$OUT
 for s in $STEPS; do
   case "$s" in
     testsvar) run gpu_tests_var 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "var or packed or zipf or mixed or every_length or smoke" ;;
+    testsbuild) run gpu_tests_build 600 python -u -m pytest tests/test_gpu_parity.py tests/test_loopback.py -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "build or loopback or verify_drops or receive_bench" ;;
     tests) run gpu_tests 900 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;        # the driver's invocation
     bench2) run bench2 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
