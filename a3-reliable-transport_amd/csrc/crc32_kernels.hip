@@ -726,8 +726,12 @@ constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read
 constexpr uint32_t kPcFlags = kPcStage + 16 * kPcSlot;  // 64 B per wave: packet-start flags
 constexpr uint32_t kPcBal = kPcFlags + 16 * 64;          // wave split: 16 piece sums, 17 u64 starts
 constexpr uint32_t kPcSpre = kPcBal + 64 + 17 * 8;       // 17 u32: pieces before each wave's range
-constexpr uint32_t kPcRem = kPcSpre + 80;                // 16 u32: pieces each wave has left, by SIMD
-constexpr uint32_t kPcLdsWords = (kPcRem + 64) / 4;      // 161,896 B
+// 16 u32: pieces each wave has left, by SIMD (read as one 16-B vector per SIMD, so the
+// base is 16-B aligned: pieces_loop takes the LDS base as a pointer, the compiler assumes
+// natural alignment, and a misaligned ds_read_b128 here cost C5 3.3 us per launch)
+constexpr uint32_t kPcRem = (kPcSpre + 17 * 4 + 15) & ~15u;
+constexpr uint32_t kPcLdsWords = (kPcRem + 64) / 4;      // 161,904 B
+static_assert(kPcRem % 16 == 0 && kPcStage % 16 == 0 && kPcSlot % 16 == 0 && kPcOps % 16 == 0, "LDS vector alignment");
 static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
 static_assert(kPcLdsWords * 4 <= 163840, "LDS");
 
