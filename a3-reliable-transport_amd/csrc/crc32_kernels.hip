@@ -121,6 +121,17 @@ __device__ __forceinline__ uint32_t op_apply(const char *lds, uint32_t base, uin
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c);
+// w ^ op_apply(base, v): each byte address is one v_bfe + one v_lshl_or, the five-way XOR
+// two v_bitop3 (the piece kernel's scan levels)
+__device__ __forceinline__ uint32_t op_apply_fold(const char *lds, uint32_t base, uint32_t v, uint32_t w) {
+    const uint32_t a0 = (__builtin_amdgcn_ubfe(v, 0, 8) << 2) | base;
+    const uint32_t a1 = (__builtin_amdgcn_ubfe(v, 8, 8) << 2) | (base + 1024u);
+    const uint32_t a2 = (__builtin_amdgcn_ubfe(v, 16, 8) << 2) | (base + 2048u);
+    const uint32_t a3 = ((v >> 24) << 2) | (base + 3072u);
+    return xor3(xor3(lds_rd(lds, a0), lds_rd(lds, a1), lds_rd(lds, a2)), lds_rd(lds, a3), w);
+}
+
 // ---- staggered 8-copy tables (conflict-free with a quarter of the replication) ------
 // A "table set" is 4 byte-tables (256 u32 each) of one linear map.  Each 32-lane half of
 // a wave is split into 4 groups of 8 lanes; in lookup instruction s, group g reads table
@@ -903,8 +914,12 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 template <class Prov>
 __device__ __forceinline__ void pieces_meta(const Prov &prov, uint64_t q0, uint64_t hi, uint32_t lane, MetaRaw &raw,
                                             __amdgpu_buffer_rsrc_t rs) {
-    const uint64_t pi = q0 + lane;
-    prov.load(pi < hi ? pi : hi - 1, raw, rs);
+    if constexpr (Prov::kGroupLoad) {
+        prov.load_group(q0, lane, raw);  // buffer loads: lanes past the arrays read 0
+    } else {
+        const uint64_t pi = q0 + lane;
+        prov.load(pi < hi ? pi : hi - 1, raw, rs);
+    }
 }
 
 // The piece-stream main loop: packets [lo, hi) of the provider (wpieces = their piece
@@ -928,12 +943,14 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
     int32_t spec = kNoSpan;        // view offset of the prefetched span
     u32x4 x[5];
     uint32_t nrounds = 0, done = 0;
-    for (uint64_t p0 = lo; p0 < hi;) {
+    hi = uniform64(hi);  // wave-uniform in SGPRs: the round's packet arithmetic stays scalar
+    for (uint64_t p0 = uniform64(lo); p0 < hi;) {
         uint64_t off;
         uint32_t len, aux = 0, oslot = 0;
         bool valid;
         prov.decode(raw, off, len, valid, aux, oslot);
-        const bool have = p0 + lane < hi;
+        const uint32_t inview = hi - p0 > 64u ? 64u : uint32_t(hi - p0);  // wave-uniform (SALU)
+        const bool have = lane < inview;
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
             len = 0;
@@ -1054,20 +1071,22 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         uint32_t W = c;
         {
             const uint32_t u = __shfl_up(W, 1);
-            if (lp >= 1u && lane >= 1u) W ^= stag_apply<128>(lds, K.kA, K.sel, u);
+            if (lp >= 1u && lane >= 1u) W = stag_apply3x<128>(lds, K.kA, K.sel, u, W);
         }
         // levels no lane needs (every packet of the round has < dd pieces in it) are
-        // skipped with a wave-uniform branch: small-packet rounds stop early
+        // skipped with a wave-uniform branch on the ballot (SGPRs): small-packet rounds
+        // stop early
 #pragma unroll
         for (uint32_t dd = 2, o = 0; dd < 64; dd <<= 1, ++o) {
-            if (__ballot(lp >= dd && lane >= dd) == 0) break;
+            const bool need = lp >= dd && lane >= dd;
+            if (__builtin_amdgcn_ballot_w64(need) == 0) break;
             const uint32_t u = __shfl_up(W, dd);
-            if (lp >= dd && lane >= dd) W ^= op_apply(lds, kPcOps + o * kOpBytes, u);
+            if (need) W = op_apply_fold(lds, kPcOps + o * kOpBytes, u, W);  // exec-masked: idle lanes issue no lookups
         }
         epi.put(pout, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
         carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
         skip = partial ? last_gp + 1 : 0u;
-        p0 = p0n;
+        p0 = uniform64(p0n);  // keeps the loop-carried packet index in SGPRs
         if (WTP_PROBE && nrounds == 0) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
         ++nrounds;
         if constexpr (Prov::kVarLen && WTP_PC_LAG) {
@@ -1078,9 +1097,11 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             done += total;
             const uint32_t left = wpieces > done ? wpieces - done : 0u;
             const uint32_t simd = wave & 3u;
-            if (lane == 0) *(__attribute__((address_space(3))) uint32_t *)((lchar *)lds + kPcRem + 4u * (4u * simd + (wave >> 2))) = left;
-            const u32x4 r4 = *(const lu32x4 *)((lchar *)lds + kPcRem + 16u * simd);
-            rotate_prio(uint32_t(r4.x < left) + uint32_t(r4.y < left) + uint32_t(r4.z < left) + uint32_t(r4.w < left));
+            typedef __attribute__((address_space(3))) uint32_t lu32w;
+            if (lane == 0) *(lu32w *)((lchar *)lds + kPcRem + 4u * (4u * simd + (wave >> 2))) = left;
+            // lanes 0..3 read the SIMD's four entries; the rank is one ballot's popcount
+            const uint32_t other = *(const lu32w *)((lchar *)lds + kPcRem + 16u * simd + 4u * (lane & 3u));
+            rotate_prio(uint32_t(__popcll(__builtin_amdgcn_ballot_w64(lane < 4u && other < left))));
         } else {
             rotate_prio(nrounds + (wave >> 2));
         }
@@ -1203,6 +1224,7 @@ typedef __attribute__((address_space(3))) uint32_t lu32;
 struct LdsIdxDgramProv {
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
+    static constexpr bool kGroupLoad = false;
     uint64_t stride;
     const uint32_t *__restrict__ rl;
     const lu32 *list;
@@ -1909,6 +1931,7 @@ namespace dev {
 struct FixedProvL {
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kGroupLoad = false;
     uint64_t stride, lead;
     uint32_t len;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
@@ -1922,12 +1945,21 @@ struct FixedProvL {
 struct ArrayProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kGroupLoad = true;  // load_group: 32-bit buffer offsets, no clamp
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
+    uint32_t n;  // packets of this launch (< 2^28: the arrays' byte extents fit 32 bits)
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
         r.a = reinterpret_cast<const uint32_t *>(offs)[2 * p];  // low dword: the view is < 2 GiB
         r.b = lens[p];
+    }
+    // packets q0 + lane: one VALU address per array; past n the loads return 0 (the range
+    // check covers voffset, so the whole offset goes there, none in soffset)
+    __device__ __forceinline__ void load_group(uint64_t q0, uint32_t lane, MetaRaw &r) const {
+        const uint32_t pi = uint32_t(q0) + lane;
+        r.a = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(offs, n * 8u), int(pi * 8u), 0, 0);
+        r.b = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(lens, n * 4u), int(pi * 4u), 0, 0);
     }
     __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
     __device__ __forceinline__ const uint32_t *len_array() const { return lens; }
@@ -1947,6 +1979,7 @@ struct ArrayProvL {
 struct DgramProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
+    static constexpr bool kGroupLoad = false;
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
@@ -2073,7 +2106,7 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
         return launch_stream(*s, b, base_bytes, d_offsets, d_lengths, n, d_out, st);
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
-        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead}, cnt,
+        rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead, uint32_t(cnt)}, cnt,
                            dev::CrcEpi{d_out + p, uint32_t(cnt)}, st);
         if (rc) break;
     }
