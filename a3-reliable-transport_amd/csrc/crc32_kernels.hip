@@ -51,22 +51,28 @@ namespace wtp {
 constexpr int kG = 16;                       // lanes per packet in the braided kernel
 constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
 constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
-constexpr int kPieceS = 64;                  // piece bytes in the general kernel
+#ifndef WTP_PC_S  // piece bytes in the general kernel (A/B builds: 128 with 512-thread blocks)
+#define WTP_PC_S 64
+#endif
+constexpr int kPieceS = WTP_PC_S;
+static_assert(kPieceS == 64 || kPieceS == 128, "piece size");
+constexpr uint32_t kHinitWords = (kPieceS + 4) & ~3;  // shift(~0, h), h = 0..kPieceS, padded
 constexpr uint32_t kMaxVarLen = 4096;
 constexpr uint64_t kSubBatch = 1ull << 28;      // packets per general-kernel launch (32-bit store offsets)        // 64 pieces x 64 B: one packet per wave max
 
 constexpr uint32_t OFF_BRAID = 0;            // 4x256 braid word tables (advance 256 B)
 constexpr uint32_t OFF_INV = 1024;           // 6 ops: x^-32, x^-64, x^-128, x^-256, x^-512, x^-1024
 constexpr uint32_t OFF_S4 = OFF_INV + 6 * 1024;   // 4x256 slice-by-4 word tables
-constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*64*d), d = 1..32
-constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..64 (head-piece init)
+constexpr uint32_t OFF_FWD = OFF_S4 + 1024;       // 6 ops: x^(8*S*d), d = 1..32 (S = kPieceS)
+constexpr uint32_t OFF_HINIT = OFF_FWD + 6 * 1024;  // shift(~0, h), h = 0..S (head-piece init)
 // k_stream (packed mixed lengths): T256 = shift by one 32-B block; 38 nibble operators
 // (8 tables x 16 words each): shift by 128 * 2^k B (k = 0..5, the lane scan), then the
 // payload-length shift in four 3-bit levels (level k, digit j: shift by j * 8^k B).
-constexpr uint32_t OFF_T256 = OFF_HINIT + 68;
+constexpr uint32_t OFF_T256 = OFF_HINIT + kHinitWords;
 constexpr uint32_t kStNibOps = 6 + 32;
 constexpr uint32_t OFF_NIB = OFF_T256 + 1024;
-constexpr uint32_t TAB_WORDS = OFF_NIB + kStNibOps * 128;
+constexpr uint32_t OFF_X64 = OFF_NIB + kStNibOps * 128;  // x^(8*64): joins the two chains of a 128-B piece
+constexpr uint32_t TAB_WORDS = OFF_X64 + 1024;
 
 // LDS images (staggered table sets are described at StagKeys below).
 constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
@@ -729,13 +735,20 @@ __device__ __forceinline__ u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off
 // holds a span of 16-B chunks with 16 B of padding after every 256 B (chunk c at
 // 16*(c + c/16)): the windows of consecutive pieces are 64 B apart, and the padding
 // spreads their 16-B reads over all bank groups instead of four.
+#ifndef WTP_PC_THREADS
+#define WTP_PC_THREADS 1024
+#endif
+constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThreads), kPcWaves = kPcThreads / 64;
+constexpr uint32_t kPcWords = uint32_t(kPieceS) / 4;                // window words per lane
+constexpr uint32_t kPcNOps = kPieceS == 64 ? 5 : 6;                  // plain scan operators in LDS
 constexpr uint32_t kPcOps = 65536;
-constexpr uint32_t kPcHinit = kPcOps + 5 * kOpBytes;
-constexpr uint32_t kPcStage = kPcHinit + 272;
-constexpr uint32_t kPcChunks = 272;  // span chunks a slot holds: 64 pieces + gaps + head slack
-constexpr uint32_t kPcSlot = 4640;   // 16 * (phys(kPcChunks) + 1): windows read one chunk past
-constexpr uint32_t kPcFlags = kPcStage + 16 * kPcSlot;  // 64 B per wave: packet-start flags
-constexpr uint32_t kPcBal = kPcFlags + 16 * 64;          // wave split: 16 piece sums, 17 u64 starts
+constexpr uint32_t kPcHinit = kPcOps + kPcNOps * kOpBytes;
+constexpr uint32_t kPcStage = kPcHinit + 4 * kHinitWords;
+constexpr uint32_t kPcChunks = 4 * uint32_t(kPieceS) + 16;  // span chunks a slot holds: 64 pieces + gaps + head slack
+constexpr uint32_t kPcSlot = 16 * (kPcChunks + kPcChunks / 16 + 1);  // windows read one chunk past
+constexpr uint32_t kPcSpanRegs = (kPcChunks + 63) / 64;     // lane-contiguous 16-B loads per span
+constexpr uint32_t kPcFlags = kPcStage + kPcWaves * kPcSlot;  // 64 B per wave: packet-start flags
+constexpr uint32_t kPcBal = kPcFlags + kPcWaves * 64;         // wave split: 16 piece sums, 17 u64 starts
 constexpr uint32_t kPcSpre = kPcBal + 64 + 17 * 8;       // 17 u32: pieces before each wave's range
 // 16 u32: pieces each wave has left, by SIMD (read as one 16-B vector per SIMD, so the
 // base is 16-B aligned: pieces_loop takes the LDS base as a pointer, the compiler assumes
@@ -787,10 +800,6 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 // call finish() (two barriers).  k_pieces runs 1024-thread blocks: the divisions by the
 // thread and wave counts are shifts (64-bit divisions by a runtime value cost ~100 VALU
 // each, and the target loop had 15 of them).
-#ifndef WTP_PC_THREADS
-#define WTP_PC_THREADS 1024
-#endif
-constexpr uint32_t kPcThreads = WTP_PC_THREADS, kPcLogT = __builtin_ctz(kPcThreads);
 #ifndef WTP_PC_LEN128
 #define WTP_PC_LEN128 1  // wave split: length words by two 16-B loads (0: eight dword loads)
 #endif
@@ -879,9 +888,10 @@ struct WaveSplit {
 // Lane-contiguous load of kPcChunks 16-B chunks starting at view offset b16 (16-aligned,
 // may be negative near the buffer start): 4 full wave instructions + 16 lanes of a
 // fifth.  Offsets outside the buffer read 0 without touching memory.
-__device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16, uint32_t lane, u32x4 (&x)[5]) {
+__device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16, uint32_t lane,
+                                          u32x4 (&x)[kPcSpanRegs]) {
 #pragma unroll
-    for (uint32_t i = 0; i < 5; ++i) {
+    for (uint32_t i = 0; i < kPcSpanRegs; ++i) {
         const uint32_t c = 64u * i + lane;
         x[i] = buf_ld16(rs, c < kPcChunks ? uint32_t(b16) + 16u * c : 0x80000000u);
     }
@@ -941,7 +951,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
     uint32_t skip = 0, carry = 0;  // pieces of packet p0 done in earlier rounds, their register
     int32_t spec = kNoSpan;        // view offset of the prefetched span
-    u32x4 x[5];
+    u32x4 x[kPcSpanRegs];
     uint32_t nrounds = 0, done = 0;
     hi = uniform64(hi);  // wave-uniform in SGPRs: the round's packet arithmetic stays scalar
     for (uint64_t p0 = uniform64(lo); p0 < hi;) {
@@ -996,7 +1006,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         const uint32_t total = outm ? uint32_t(__builtin_ctzll(outm)) : 64u;  // >= 1: lane 0 fits
         const bool active = lane < total;
         const int32_t vf0 = int32_t(poff) - ws;  // bytes of the window before the packet
-        const int32_t vf = active ? (vf0 > 64 ? 64 : vf0) : 64;
+        const int32_t vf = active ? (vf0 > kPieceS ? kPieceS : vf0) : kPieceS;
 
         // --- stage the span ---------------------------------------------------------------
         const bool hit = __ballot(active && (ws < spec || we - spec > kSpanBytes)) == 0;
@@ -1007,18 +1017,18 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the miss pays its latency here
         }
 #pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
-        if (lane < kPcChunks - 256u) *(lu32x4 *)(slot + stage_addr(256u + lane)) = x[4];
+        for (uint32_t i = 0; i + 1 < kPcSpanRegs; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
+        if (lane < kPcChunks - 64u * (kPcSpanRegs - 1)) *(lu32x4 *)(slot + stage_addr(64u * (kPcSpanRegs - 1) + lane)) = x[kPcSpanRegs - 1];
         __builtin_amdgcn_wave_barrier();
         // the window's five 16-B blocks, aligned (dword-aligned variants without the
         // rotation below were slower on C5: ds_read2_b32 pairs at the 64-B lane stride
         // conflict 4-way, +13%; unaligned ds_read_b128 from inline asm, which gfx950
         // executes correctly, +39%)
-        uint32_t d[20];
+        uint32_t d[kPcWords + 4];
         {
             const uint32_t blk = active ? uint32_t(ws - sbase) >> 4 : 0u;
 #pragma unroll
-            for (uint32_t u = 0; u < 5; ++u) {
+            for (uint32_t u = 0; u < kPcWords / 4 + 1; ++u) {
                 const u32x4 y = *(const lu32x4 *)(slot + stage_addr(blk + u));
                 d[4 * u + 0] = y.x;
                 d[4 * u + 1] = y.y;
@@ -1043,16 +1053,23 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
         const uint32_t a = uint32_t(ws) & 15u;
         const uint32_t m2 = 0u - ((a >> 3) & 1u), m1 = 0u - ((a >> 2) & 1u), sb = a & 3u;
-        uint32_t e[18];
+        uint32_t e[kPcWords + 2];
 #pragma unroll
-        for (int i = 0; i < 18; ++i) e[i] = d[i] ^ ((d[i] ^ d[i + 2]) & m2);
+        for (int i = 0; i < int(kPcWords) + 2; ++i) e[i] = d[i] ^ ((d[i] ^ d[i + 2]) & m2);
 #pragma unroll
-        for (int i = 0; i < 17; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
+        for (int i = 0; i < int(kPcWords) + 1; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
 
-        uint32_t c = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
+        // one chain per 64 B of the window (128-B pieces: two independent chains, joined
+        // below by x^(8*64))
+        constexpr int kChains = int(kPcWords) / 16;
+        uint32_t cc[kChains];
+        cc[0] = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
+        if constexpr (kChains == 2) cc[1] = 0u;
         const int32_t vf8 = 8 * vf;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int j = 0; j < 16 * kChains; ++j) {
+            const int i = (j % kChains) * 16 + j / kChains;  // interleave the chains
+            uint32_t &c = cc[j % kChains];
             const uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
             // keep the bytes at window offset >= vf: the low s = clamp(8 vf - 32 i, 0, 32)
             // bits of word i go.  One v_med3 + one v_lshlrev_b64 (the shift unit reads 6
@@ -1063,7 +1080,9 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             const uint32_t keep = (i & 1) ? uint32_t(k64 >> 32) : uint32_t(k64);
             c = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(c, wd, keep, 0x78));  // c ^ (wd & keep)
         }
-        // head piece: R_~0(head) = R_0(0^vf || head) ^ shift(~0, 64 - vf)
+        uint32_t c = cc[0];
+        if constexpr (kChains == 2) c = stag_apply3x<128>(lds, K.kA, K.sel, cc[0], cc[1]);  // x^(8*64) * c0 ^ c1
+        // head piece: R_~0(head) = R_0(0^vf || head) ^ shift(~0, S - vf)
         const uint32_t hw = lds_rd(lds, kPcHinit + 4u * uint32_t(kPieceS - (vf < 0 ? 0 : vf)));
         c ^= gp == 0u ? hw : 0u;
 
@@ -1071,7 +1090,11 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         uint32_t W = c;
         {
             const uint32_t u = __shfl_up(W, 1);
-            if (lp >= 1u && lane >= 1u) W = stag_apply3x<128>(lds, K.kA, K.sel, u, W);
+            if constexpr (kPieceS == 64) {  // x^(8*64) is the staggered set 1
+                if (lp >= 1u && lane >= 1u) W = stag_apply3x<128>(lds, K.kA, K.sel, u, W);
+            } else {  // set 1 joins the chains; x^(8*128) is plain operator 0
+                if (lp >= 1u && lane >= 1u) W = op_apply_fold(lds, kPcOps, u, W);
+            }
         }
         // levels no lane needs (every packet of the round has < dd pieces in it) are
         // skipped with a wave-uniform branch on the ballot (SGPRs): small-packet rounds
@@ -1081,7 +1104,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             const bool need = lp >= dd && lane >= dd;
             if (__builtin_amdgcn_ballot_w64(need) == 0) break;
             const uint32_t u = __shfl_up(W, dd);
-            if (need) W = op_apply_fold(lds, kPcOps + o * kOpBytes, u, W);  // exec-masked: idle lanes issue no lookups
+            if (need) W = op_apply_fold(lds, kPcOps + (o + kPcNOps - 5) * kOpBytes, u, W);  // exec-masked: idle lanes issue no lookups
         }
         epi.put(pout, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
         carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
@@ -1101,7 +1124,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             if (lane == 0) *(lu32w *)((lchar *)lds + kPcRem + 4u * (4u * simd + (wave >> 2))) = left;
             // lanes 0..3 read the SIMD's four entries; the rank is one ballot's popcount
             const uint32_t other = *(const lu32w *)((lchar *)lds + kPcRem + 16u * simd + 4u * (lane & 3u));
-            rotate_prio(uint32_t(__popcll(__builtin_amdgcn_ballot_w64(lane < 4u && other < left))));
+            rotate_prio(uint32_t(__popcll(__builtin_amdgcn_ballot_w64(lane < kPcWaves / 4u && other < left))));
         } else {
             rotate_prio(nrounds + (wave >> 2));
         }
@@ -1117,19 +1140,19 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
 // store() writes LDS; a barrier must follow before pieces_loop.
 template <int THREADS>
 struct PcTables {
-    static constexpr uint32_t kOpQ = 5 * 256, kOpPer = (kOpQ + THREADS - 1) / THREADS;
+    static constexpr uint32_t kOpQ = kPcNOps * 256, kOpPer = (kOpQ + THREADS - 1) / THREADS;
     StagFill<2, THREADS> fill;
     u32x4 q[kOpPer];
     uint32_t hv;
     __device__ __forceinline__ static void sets(const uint32_t *gtab, StagSet (&s)[2]) {
         s[0] = {gtab + OFF_S4, 0u};
-        s[1] = {gtab + OFF_FWD, 128u};
+        s[1] = {gtab + (kPieceS == 64 ? OFF_FWD : OFF_X64), 128u};  // x^(8*64)
     }
     __device__ __forceinline__ void load(const uint32_t *gtab) {
         StagSet ss[2];
         sets(gtab, ss);
         fill.load(ss);
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(gtab + OFF_FWD + 1024 * (6 - kPcNOps));
 #pragma unroll
         for (uint32_t k = 0; k < kOpPer; ++k) {
             const uint32_t i = threadIdx.x + k * THREADS;
@@ -1216,7 +1239,7 @@ constexpr uint32_t kVfCap = (kPcFlags - kVfList) / 4;
 constexpr uint32_t kVfCtl = (kPcLdsWords * 4 + 15) & ~15u;
 constexpr uint32_t kVfPer = 8;                          // packets rescanned per thread and pass
 constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
-static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fix-up LDS");
+static_assert(WTP_PC_S != 64 || (kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4), "verify fix-up LDS");
 
 typedef __attribute__((address_space(3))) uint32_t lu32;
 
@@ -1766,6 +1789,7 @@ std::vector<uint32_t> host_tables() {
         make_operator(&t[OFF_FWD + 1024 * o], [&](uint32_t v) { return shift_bytes(v, nb); });
     }
     for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
+    make_operator(&t[OFF_X64], [](uint32_t v) { return shift_bytes(v, 64); });
     make_operator(&t[OFF_T256], [](uint32_t v) { return shift_bytes(v, 32); });
     auto nib = [&](uint32_t op, uint64_t nbytes) {
         for (uint32_t i = 0; i < 8; ++i)
