@@ -1239,6 +1239,8 @@ constexpr uint32_t kVfCap = (kPcFlags - kVfList) / 4;
 constexpr uint32_t kVfCtl = (kPcLdsWords * 4 + 15) & ~15u;
 constexpr uint32_t kVfPer = 8;                          // packets rescanned per thread and pass
 constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
+// (WTP_PC_S=128 is an A/B build of k_pieces only: its 8-wave slot layout leaves the verify
+// fix-up no room for its list, so that build must not be used for datagrams that need it)
 static_assert(WTP_PC_S != 64 || (kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4), "verify fix-up LDS");
 
 typedef __attribute__((address_space(3))) uint32_t lu32;
