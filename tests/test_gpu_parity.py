@@ -1029,6 +1029,7 @@ def test_build_data_packets_paths(W, total, stride, pay_off, wire_off, with_len,
     (1456 * 1000, 1488, True, False, False, 0xFFFFFFF0),  # wider slots, no lengths, seq wraps
     (1456 * 10 + 1, 1500, False, True, True, 1),         # stride % 16 != 0: the three-step path
     (100, 1472, True, True, True, 0),                    # one short datagram
+    (1456 * 100 + 5, 1500, True, True, True, 7),         # zero copy into 1500-B slots: the three-step path over host memory
 ])
 @pytest.mark.parametrize("zero_copy", ["1", "0"])
 def test_host_build_data_packets(W, total, stride, pin_src, pin_wire, with_len, seq0, zero_copy):
