@@ -119,17 +119,12 @@ __device__ __forceinline__ uint32_t lds_rd(const char *lds, uint32_t byte_addr) 
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
 
-// Linear operator stored as 4 byte tables at LDS byte offset `base`.
-__device__ __forceinline__ uint32_t op_apply(const char *lds, uint32_t base, uint32_t v) {
-    return (lds_rd(lds, base + ((v & 0xFFu) << 2)) ^ lds_rd(lds, base + 1024u + ((v >> 6) & 0x3FCu))) ^
-           (lds_rd(lds, base + 2048u + ((v >> 14) & 0x3FCu)) ^ lds_rd(lds, base + 3072u + ((v >> 22) & 0x3FCu)));
-}
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c);
-// w ^ op_apply(base, v): each byte address is one v_bfe + one v_lshl_or, the five-way XOR
-// two v_bitop3 (the piece kernel's scan levels)
+// w ^ f(v) for a linear operator f stored as 4 byte tables (256 words each) at LDS byte
+// offset base: each byte address is one v_bfe + one v_lshl_or, the five-way XOR two
+// v_bitop3 (the piece kernel's scan levels)
 __device__ __forceinline__ uint32_t op_apply_fold(const char *lds, uint32_t base, uint32_t v, uint32_t w) {
     const uint32_t a0 = (__builtin_amdgcn_ubfe(v, 0, 8) << 2) | base;
     const uint32_t a1 = (__builtin_amdgcn_ubfe(v, 8, 8) << 2) | (base + 1024u);
