@@ -51,7 +51,8 @@ namespace wtp {
 constexpr int kG = 16;                       // lanes per packet in the braided kernel
 constexpr int kBraids = 4 * kG;              // 64 braids x 4-byte words
 constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
-#ifndef WTP_PC_S  // piece bytes in the general kernel (A/B builds: 128 with 512-thread blocks)
+#ifndef WTP_PC_S  // piece bytes in the general kernel (128 was an A/B variant; it no
+                  // longer compiles: the verify fix-up's LDS static_assert below rejects it)
 #define WTP_PC_S 64
 #endif
 constexpr int kPieceS = WTP_PC_S;
@@ -874,8 +875,15 @@ struct WaveSplit {
         }
         if (threadIdx.x == 0) spre[nw] = total;
         __syncthreads();
-        lo = uniform64(starts[wave]);
-        hi = uniform64(starts[wave + 1]);
+        // Every starts[w] was written above: pieces_of_len() >= 1, so total >= g1 - g0 > 0
+        // and each target < total lies in exactly one thread's [excl, excl + sum).  The
+        // clamp keeps a wave inside [g0, g1] even if that invariant were ever broken: a
+        // round-3 development build counted 0 pieces for small packets, so an all-small
+        // workgroup wrote no starts[1..15] and its waves ran over the previous kernel's
+        // stale LDS indices (hipErrorIllegalAddress).
+        const uint64_t s0 = uniform64(starts[wave]), s1 = uniform64(starts[wave + 1]);
+        lo = s0 < g0 ? g0 : (s0 > g1 ? g1 : s0);
+        hi = s1 < lo ? lo : (s1 > g1 ? g1 : s1);
         wpieces = uint32_t(__builtin_amdgcn_readfirstlane(int(spre[wave + 1] - spre[wave])));
     }
 };
@@ -1234,9 +1242,22 @@ constexpr uint32_t kVfCap = (kPcFlags - kVfList) / 4;
 constexpr uint32_t kVfCtl = (kPcLdsWords * 4 + 15) & ~15u;
 constexpr uint32_t kVfPer = 8;                          // packets rescanned per thread and pass
 constexpr uint32_t kVfPass = kVfWaves * 64 * kVfPer;   // packets rescanned per pass
-// (WTP_PC_S=128 is an A/B build of k_pieces only: its 8-wave slot layout leaves the verify
-// fix-up no room for its list, so that build must not be used for datagrams that need it)
-static_assert(WTP_PC_S != 64 || (kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4), "verify fix-up LDS");
+// Unconditional: a layout that leaves the fix-up list no room (e.g. the rejected 128-B
+// piece variant) must not compile, rather than overwrite the flags with indices.
+static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fix-up LDS");
+
+// Product builds (a3-reliable-transport_amd/Makefile) take every A/B, probe and ablation
+// knob of this file at its shipped value; only tools/build_ab.sh and tools/Makefile (kbench,
+// pprobe) define WTP_AB_BUILD to build variants.  A misconfigured product build is a
+// compile error, not a library that runs wrong.
+#ifndef WTP_AB_BUILD
+static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1,
+              "product build: piece-kernel knobs must keep their shipped values");
+static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
+static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
+                  WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
+              "product build: fused-builder knobs must keep their shipped values");
+#endif
 
 typedef __attribute__((address_space(3))) uint32_t lu32;
 

@@ -74,3 +74,127 @@ def test_host_cores_reports_affinity_and_model():
     hc = bench.host_cores()
     assert 1 <= hc["threads"] <= hc["affinity_cpus"] == len(os.sched_getaffinity(0))
     assert "model" in hc
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _FakeW:
+    """CPU stand-in for the binding (the oracle computes the CRCs): runs bench.py's legs
+    through their real control flow without a GPU.  Test infrastructure only."""
+
+    def __init__(self, O):
+        self.O, self.reserved, self.launches = O, [], 0
+
+    def synth_fill(self, out, start_byte=0, seed=0x5EED, nbytes=None, stream=None):
+        import torch
+        out[:nbytes] = torch.from_numpy(self.O.synth_fill_np(nbytes, start_byte=start_byte))
+
+    def crc32_batch_fixed(self, buf, stride, length, n, out, stream=None):
+        import torch
+        self.launches += 1
+        v = self.O.batch_fixed(buf.numpy()[:n * stride], stride, length, n)
+        out.copy_(torch.from_numpy(v.view(np.int32)))
+
+    def reserve_cus(self, k, device=0):
+        self.reserved.append(k)
+
+
+class _FakeEvent:
+    def record(self, stream):
+        import time
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
+def _fake_settle(step, stream, w_req, **kw):
+    for _ in range(3):
+        step()
+    return 3, []
+
+
+def _no_gpu(monkeypatch, bench):
+    import torch
+    monkeypatch.setattr(bench, "TimingEvent", _FakeEvent)
+    monkeypatch.setattr(bench, "settle", _fake_settle)
+    monkeypatch.setattr(torch.cuda, "Stream", lambda: "crc-stream")
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda: "default-stream")
+    monkeypatch.setattr(torch.cuda, "set_stream", lambda s: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+
+
+def test_n1_extra_legs_fields_on_cpu(monkeypatch):
+    """The two legs the N = 1 line carries after its timed region: alt_buffer (two 1 M
+    buffers in turn) and c4_shard_1gpu (the N > 1 pipelined step with a one-rank gather,
+    here over gloo): fields, sizes, the CU reservation restored, and the gathered vector
+    equal to the oracle's over the same packets (small n: the real leg runs 2 M)."""
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "a3-reliable-transport_amd"))
+    import oracle as O
+    import shard
+    _no_gpu(monkeypatch, bench)
+    W = _FakeW(O)
+    n = 3000
+    nbytes = n * bench.PAYLOAD
+    buf = torch.zeros(nbytes + 64, dtype=torch.uint8)
+    W.synth_fill(buf, nbytes=nbytes)
+    alt = bench.alt_buffer_leg(W, buf, nbytes, n, "cpu", "default-stream", steps=4, warmup=5)
+    assert alt["steps"] == 4 and alt["alt_buffer_kernel_ms"] == alt["kernel_ms_mean"] > 0
+    assert {"GBs", "frac", "kernel_ms_median", "step_ms"} <= set(alt)
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        W.launches = 0
+        c4 = bench.c4_shard_leg(W, shard, "cpu", 0, steps=4, warmup=5, n=n)
+    finally:
+        dist.destroy_process_group()
+    assert c4["packets"] == n and c4["bytes_per_launch"] == nbytes and c4["steps"] == 4
+    assert W.reserved == [8, 0]  # 8 CUs for the gather while the leg runs, then restored
+    assert W.launches == 3 + 4  # settle + the timed steps, one launch each
+    want = O.batch_fixed(O.synth_fill_np(nbytes), bench.PAYLOAD, bench.PAYLOAD, n)
+    assert c4["sha256"] == hashlib.sha256(want.astype("<u4").tobytes()).hexdigest()[:16]
+    assert c4["parity_match"] is None  # no reference digest at this size; the real leg has one
+    assert {"kernel_ms_mean", "GBs", "frac", "step_ms", "value_GiBs"} <= set(c4)
+
+
+def test_default_c4_leg_is_the_two_million_packet_shard():
+    import inspect
+
+    import bench
+    sig = inspect.signature(bench.c4_shard_leg)
+    assert sig.parameters["n"].default == 2097152 == bench.C4_PACKETS // 8
+
+
+def test_traffic_null_unless_kernel_code_matches(tmp_path):
+    """roofline.traffic is the committed PMC pass's number only while the shipped
+    k_fixed_braid<6> has the code that pass measured: one flipped byte of the recorded
+    hash gives traffic null."""
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "a3-reliable-transport_amd"))
+    import wtp_crc32 as W
+    rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    v, info = bench.pmc_traffic(1 << 20, W.LIB_PATH)
+    assert v == rec["hbm_bytes_per_launch"] and info["status"].startswith("measured"), info
+    h = rec["kernel_code"]["sha256"]
+    rec["kernel_code"]["sha256"] = ("0" if h[0] != "0" else "1") + h[1:]
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(rec))
+    v, info = bench.pmc_traffic(1 << 20, W.LIB_PATH, str(p))
+    assert v is None and info["status"].startswith("stale"), info
+    v, info = bench.pmc_traffic(2 << 20, W.LIB_PATH)
+    assert v is None

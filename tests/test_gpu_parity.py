@@ -248,6 +248,15 @@ def test_var_wave_split_skewed(W, VAR, n):
     _var_check(VAR, lens, seed=n)
 
 
+def test_var_all_tiny_workgroups(W, VAR):
+    """Every workgroup's packets are 0 or 1 B (70 K packets, ~270 per workgroup): the
+    case that faulted a round-3 development build (a split that counted such
+    packets as 0 pieces left the wave ranges to stale LDS).  In the shipped split every
+    packet is >= 1 piece and the wave ranges are clamped to the workgroup's packets."""
+    rng = np.random.default_rng(70_000)
+    _var_check(VAR, rng.integers(0, 2, 70_000).astype(np.uint32), seed=7)
+
+
 def test_mixed_golden_digest(W, VAR, golden):
     lens = np.array([1 + (i * 7919) % 1456 for i in range(2048)], dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)

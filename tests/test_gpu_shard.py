@@ -171,3 +171,24 @@ def test_bench_c4_shard_gather_one_rank(W):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["config"]["packets_per_rank"] == 2097152 and line["config"]["gather"]
     assert line["parity"]["packets"] == 2097152 and line["parity"]["match"] is True, line["parity"]
+
+
+def test_bench_n1_line_carries_equal_work_c4_leg(W):
+    """The default N = 1 line (the driver's invocation, shortened): the metric's 1 M
+    packets, plus c4_shard_1gpu — rank 0's 2 M-packet C4 shard through the N > 1 pipelined
+    step with a one-rank RCCL gather, its gathered vector equal to the reference's 2 M
+    digest — and alt_buffer; roofline.traffic is reported for the shipped kernel code."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "5", "--warmup", "5",
+                        "--no-cpu-baseline", "--no-probe"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["config"]["packets_per_rank"] == 1 << 20 and line["parity"]["match"] is True
+    c4 = line["c4_shard_1gpu"]
+    assert c4["packets"] == 2097152 and c4["parity_match"] is True, c4
+    assert c4["steps"] == 5 and 0 < c4["kernel_ms_mean"] <= c4["step_ms"] * 1.5
+    assert line["alt_buffer_kernel_ms"] == line["alt_buffer"]["kernel_ms_mean"] > 0
+    assert line["roofline"]["traffic"] is not None, line["roofline"]["traffic_check"]

@@ -67,6 +67,18 @@ for s in $STEPS; do
              v=$(basename "$lib" .so)
              WTP_LIB="$ROOT/$lib" run "ab_$v" 300 python tools/bench_configs.py --only "${CFG_ONLY:-c5}" --out "$OUT/ab_$v.json"
            done ;;
+    listavail) run listavail 120 rocprofv3 --list-avail ;;
+    recvsmall) for m in cpu gpu; do for b in ${RECV_BATCHES:-1 10 64}; do
+             P=$((20000 + RANDOM % 20000))
+             timeout -k 10 60 ./a3-reliable-transport_amd/bin/wReceiver --bench 3 -p $P --crc $m --batch $b \
+               > "$OUT/recv_${m}_${b}.json" 2> "$OUT/recv_${m}_${b}.err" &
+             RP=$!; sleep 0.5
+             timeout -k 10 30 ./a3-reliable-transport_amd/bin/wBlast -h 127.0.0.1 -p $P --seconds 3 --batch ${BLAST_BATCH:-64} \
+               --corrupt 100 > "$OUT/blast_${m}_${b}.json" 2>&1
+             wait $RP; rc=$?
+             echo "recv $m $b rc=$rc: $(cat "$OUT/recv_${m}_${b}.json")" | tee -a "$OUT/steps.log"
+             if fatal "$rc"; then echo "FATAL rc=$rc in recv"; exit "$rc"; fi
+           done; done ;;
     split) run split 300 python tools/split_probe.py ;;
     footprint) run footprint 300 python tools/footprint_probe.py ;;
     copyprobe) run copyprobe 120 ./tools/bin/copyprobe ;;
