@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -67,12 +68,21 @@ class Log {
 // reference's one-call-per-packet crc32().
 class Checksums {
    public:
+    // Receiver batches of at most this many payload bytes are verified on the CPU in GPU
+    // mode (crc32_fast): below it one GPU call (launch + sync, ~25 us from the host)
+    // costs more than hashing the bytes here.  Measured crossover on the MI355X box:
+    // DESIGN.md 5 (tools/verify_crossover.cpp); WTP_VERIFY_CPU_MAX_BYTES overrides it
+    // (0 = always the GPU).
+    static constexpr size_t kCpuVerifyMaxBytes = 64 * 1024;
+
     // gpus: devices the sender spreads its file over (0 = every visible device).
-    explicit Checksums(const std::string &mode, int gpus = 1) : gpu_(mode == "gpu"), gpus_(gpus) {
+    explicit Checksums(const std::string &mode, int gpus = 1)
+        : gpu_(mode == "gpu"), gpus_(gpus), cpu_max_(cpu_max_from_env()) {
         if (mode != "gpu" && mode != "cpu") throw std::runtime_error("--crc must be cpu or gpu");
         if (gpu_ && wtp_init(0) != WTP_OK) throw std::runtime_error(std::string("GPU CRC unavailable: ") + wtp_last_error());
     }
     bool gpu() const { return gpu_; }
+    size_t cpu_verify_max_bytes() const { return cpu_max_; }
 
     // Sender build: crc of every kMaxPayload chunk of the file (Sender.cpp:88-92).  With
     // several GPUs the chunks split into one contiguous range per device (one PCIe link
@@ -93,40 +103,42 @@ class Checksums {
         return out;
     }
 
-    // Receiver verify (Receiver.cpp:203-206): CRC over datagram bytes [16, len).  Only
-    // DATA datagrams are CRC-checked by the reference (Receiver.cpp:139-206).
-    bool verify(const uint8_t *dgram, size_t len) const {
-        if (len < kHeaderBytes) return false;
-        if (gpu_) {
-            uint32_t rl = uint32_t(len), crc = 0;
-            uint8_t ok = 0;
-            if (wtp_crc32_host_verify(dgram, len, &rl, 1, &ok, &crc) != WTP_OK)
-                throw std::runtime_error(std::string("wtp_crc32_host_verify: ") + wtp_last_error());
-            return ok != 0;
-        }
-        return get_header(dgram).checksum == crc32(dgram + kHeaderBytes, len - kHeaderBytes);
-    }
-
-    // Batched receiver verify: datagram i = ring[i*stride, +rl[i]).
-    // GPU mode verifies the whole batch in one call (the ring is pinned, so the library
-    // copies it to the device with one DMA); CPU mode is one crc32() per datagram.
-    void verify_batch(const uint8_t *ring, size_t stride, const uint32_t *rl, size_t n, uint8_t *ok) const {
-        if (!n) return;
-        if (gpu_) {
+    // Batched receiver verify (Receiver.cpp:25-35,203-206): datagram
+    // i = ring[i*stride, +rl[i]), ok[i] = its CRC over bytes [16, rl[i]) equals the
+    // header's checksum.  GPU mode sends the batch to the MI355X in one call when it
+    // carries more than cpu_verify_max_bytes() of payload, and hashes it here with
+    // crc32_fast otherwise (the window-size batches of config C1); CPU mode is the
+    // reference's one byte-loop crc32() per datagram.  All routes give the same ok[].
+    // Returns true if the batch went to the GPU.
+    bool verify_batch(const uint8_t *ring, size_t stride, const uint32_t *rl, size_t n, uint8_t *ok) const {
+        if (!n) return false;
+        if (gpu_ && payload_bytes(stride, rl, n) > cpu_max_) {
             if (wtp_crc32_host_verify(ring, stride, rl, n, ok, nullptr) != WTP_OK)
                 throw std::runtime_error(std::string("wtp_crc32_host_verify: ") + wtp_last_error());
-            return;
+            return true;
         }
         for (size_t i = 0; i < n; ++i) {
             const uint8_t *d = ring + i * stride;
-            ok[i] = rl[i] >= kHeaderBytes && rl[i] <= stride &&
-                    get_header(d).checksum == crc32(d + kHeaderBytes, rl[i] - kHeaderBytes);
+            const bool shaped = rl[i] >= kHeaderBytes && rl[i] <= stride;
+            ok[i] = shaped && get_header(d).checksum == (gpu_ ? crc32_fast(d + kHeaderBytes, rl[i] - kHeaderBytes)
+                                                              : crc32(d + kHeaderBytes, rl[i] - kHeaderBytes));
         }
+        return false;
     }
 
    private:
+    static size_t payload_bytes(size_t stride, const uint32_t *rl, size_t n) {
+        size_t b = 0;
+        for (size_t i = 0; i < n; ++i) b += rl[i] > kHeaderBytes ? std::min<size_t>(rl[i], stride) - kHeaderBytes : 0;
+        return b;
+    }
+    static size_t cpu_max_from_env() {
+        const char *e = std::getenv("WTP_VERIFY_CPU_MAX_BYTES");
+        return e && *e ? size_t(std::strtoull(e, nullptr, 10)) : kCpuVerifyMaxBytes;
+    }
     bool gpu_;
     int gpus_;
+    size_t cpu_max_;
 };
 
 // Receive ring for recvmmsg: `slots` datagram slots of kSlot = 1504 bytes in pinned host
@@ -144,24 +156,12 @@ class RecvRing {
     // batches up to 4 MiB are read by the kernel in place, larger ones take one DMA per
     // slab); otherwise plain page-aligned memory (CPU verify needs no device).
     RecvRing(size_t slots, bool pinned)
-        : n_(slots), pinned_(pinned),
-          buf_(static_cast<uint8_t *>(pinned ? wtp_host_alloc(slots * kSlot) : std::aligned_alloc(4096, round4k(slots * kSlot)))),
-          len_(static_cast<uint32_t *>(pinned ? wtp_host_alloc(slots * 4) : std::aligned_alloc(4096, round4k(slots * 4)))),
+        : n_(slots), buf_(alloc<uint8_t>(slots * kSlot, pinned)), len_(alloc<uint32_t>(slots * 4, pinned)),
           ok_(slots), iov_(slots), msg_(slots), peer_(slots) {
-        if (!buf_ || !len_) throw std::runtime_error("receive ring allocation failed");
         for (size_t i = 0; i < n_; ++i) {
-            iov_[i] = {buf_ + i * kSlot, kRecv};
+            iov_[i] = {buf_.get() + i * kSlot, kRecv};
             msg_[i].msg_hdr.msg_iov = &iov_[i];
             msg_[i].msg_hdr.msg_iovlen = 1;
-        }
-    }
-    ~RecvRing() {
-        if (pinned_) {
-            wtp_host_free(buf_);
-            wtp_host_free(len_);
-        } else {
-            std::free(buf_);
-            std::free(len_);
         }
     }
     RecvRing(const RecvRing &) = delete;
@@ -177,22 +177,39 @@ class RecvRing {
         }
         const int got = ::recvmmsg(fd, msg_.data(), unsigned(n_), MSG_WAITFORONE, nullptr);
         if (got <= 0) return 0;
-        for (int i = 0; i < got; ++i) len_[i] = uint32_t(msg_[i].msg_len);  // <= kRecv (truncated like recvfrom)
+        for (int i = 0; i < got; ++i) len_.get()[i] = uint32_t(msg_[i].msg_len);  // <= kRecv (truncated like recvfrom)
         return size_t(got);
     }
-    uint8_t *slot(size_t i) { return buf_ + i * kSlot; }
-    uint32_t len(size_t i) const { return len_[i]; }
-    const uint32_t *lens() const { return len_; }
+    uint8_t *slot(size_t i) { return buf_.get() + i * kSlot; }
+    uint32_t len(size_t i) const { return len_.get()[i]; }
+    const uint32_t *lens() const { return len_.get(); }
     uint8_t *ok() { return ok_.data(); }
     const sockaddr_in &peer(size_t i) const { return peer_[i]; }
-    uint8_t *ring() { return buf_; }
+    uint8_t *ring() { return buf_.get(); }
 
    private:
-    static size_t round4k(size_t b) { return (b + 4095) & ~size_t(4095); }
+    // Each allocation is owned as soon as it exists, so a failure of the second one (or
+    // of anything later in the constructor) frees the first: pinned memory does not leak.
+    struct Free {
+        bool pinned;
+        void operator()(void *p) const {
+            if (pinned)
+                wtp_host_free(p);
+            else
+                std::free(p);
+        }
+    };
+    template <class T>
+    using Owned = std::unique_ptr<T, Free>;
+    template <class T>
+    static Owned<T> alloc(size_t bytes, bool pinned) {
+        void *p = pinned ? wtp_host_alloc(bytes) : std::aligned_alloc(4096, (bytes + 4095) & ~size_t(4095));
+        if (!p) throw std::runtime_error("receive ring allocation failed");
+        return Owned<T>(static_cast<T *>(p), Free{pinned});
+    }
     size_t n_;
-    bool pinned_;
-    uint8_t *buf_;
-    uint32_t *len_;  // recv_len per slot (pinned with the ring)
+    Owned<uint8_t> buf_;
+    Owned<uint32_t> len_;  // recv_len per slot (pinned with the ring)
     std::vector<uint8_t> ok_;
     std::vector<iovec> iov_;
     std::vector<mmsghdr> msg_;

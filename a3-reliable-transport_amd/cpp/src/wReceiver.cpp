@@ -21,8 +21,9 @@
 //
 // Batched receive: datagrams arrive through recvmmsg into a pinned
 // ring of --batch slots (default: the window size), the whole batch is verified with one
-// call (one GPU launch with --crc gpu), then processed in arrival order exactly as
-// one-at-a-time reception would.  --bench measures that path alone: it receives DATA
+// call (one GPU launch with --crc gpu; batches of at most Checksums::kCpuVerifyMaxBytes
+// of payload are hashed on the CPU with crc32_fast instead, where a GPU call's launch and
+// sync cost more), then processed in arrival order exactly as one-at-a-time reception would.  --bench measures that path alone: it receives DATA
 // datagrams (e.g. from wBlast) for the given seconds, verifying each batch on a worker
 // thread while the next one arrives, and prints one JSON line with the rate.
 #include <time.h>
@@ -62,7 +63,7 @@ int bench(int fd, const Checksums &crc, size_t batch, double seconds) {
     set_rcv_timeout_ms(fd, 500);
     RecvRing ring0(batch, crc.gpu()), ring1(batch, crc.gpu());
     RecvRing *rings[2] = {&ring0, &ring1};
-    uint64_t dgrams = 0, bytes = 0, good = 0, batches = 0;
+    uint64_t dgrams = 0, bytes = 0, good = 0, batches = 0, gpu_batches = 0;
     double t0 = 0, t1 = 0, tverify = 0;
 
     std::mutex mu;
@@ -82,7 +83,7 @@ int bench(int fd, const Checksums &crc, size_t batch, double seconds) {
                 n = job_n;
             }
             const double tv = now_s();
-            crc.verify_batch(r->ring(), RecvRing::kSlot, r->lens(), n, r->ok());
+            const bool on_gpu = crc.verify_batch(r->ring(), RecvRing::kSlot, r->lens(), n, r->ok());
             const double dv = now_s() - tv;
             uint64_t b = 0, g = 0;
             for (size_t i = 0; i < n; ++i) {
@@ -95,6 +96,7 @@ int bench(int fd, const Checksums &crc, size_t batch, double seconds) {
             bytes += b;
             good += g;
             ++batches;
+            gpu_batches += on_gpu ? 1 : 0;
             job = nullptr;
             busy = false;
             cv.notify_all();
@@ -129,10 +131,12 @@ int bench(int fd, const Checksums &crc, size_t batch, double seconds) {
     const double dt = t1 > t0 ? t1 - t0 : 1e-9;
     std::printf("{\"mode\": \"%s\", \"batch_slots\": %zu, \"datagrams\": %llu, \"payload_bytes\": %llu, "
                 "\"seconds\": %.4f, \"GBps\": %.4f, \"datagrams_per_s\": %.0f, \"ok\": %llu, \"batches\": %llu, "
-                "\"verify_seconds\": %.4f, \"verify_GBps\": %.3f, \"overlapped\": true}\n",
+                "\"verify_seconds\": %.4f, \"verify_GBps\": %.3f, \"gpu_batches\": %llu, "
+                "\"cpu_verify_max_bytes\": %zu, \"overlapped\": true}\n",
                 crc.gpu() ? "gpu" : "cpu", batch, (unsigned long long)dgrams, (unsigned long long)bytes, dt,
                 double(bytes) / dt / 1e9, double(dgrams) / dt, (unsigned long long)good, (unsigned long long)batches,
-                tverify, tverify > 0 ? double(bytes) / tverify / 1e9 : 0.0);
+                tverify, tverify > 0 ? double(bytes) / tverify / 1e9 : 0.0, (unsigned long long)gpu_batches,
+                crc.gpu() ? crc.cpu_verify_max_bytes() : size_t(0));
     return 0;
 }
 

@@ -170,14 +170,27 @@ int main(int argc, char **argv) {
         const InputFile file(a.get("input"), crc.gpu());
 
         // Every DATA datagram built on the device (--crc gpu, one device), else every DATA
-        // checksum in one batch (the device path when --crc gpu --gpus N).
-        const bool fused = crc.gpu() && std::stoi(a.get("gpus", "1")) == 1;
+        // checksum in one batch (the device path when --crc gpu --gpus N).  The wire buffer
+        // pins a second copy of the file (n * 1472 B); if it cannot be pinned or built, or
+        // is larger than WTP_WIRE_MAX_BYTES, the sender falls back to the checksum batch
+        // (crc.chunks) and writes each header per send, as with --gpus N.
+        bool fused = crc.gpu() && std::stoi(a.get("gpus", "1")) == 1;
         std::unique_ptr<WireBuffer> built;
         std::vector<uint32_t> sums;
-        if (fused)
-            built = std::make_unique<WireBuffer>(file);
-        else
-            sums = crc.chunks(file.data(), file.size());
+        if (fused) {
+            const char *cap = std::getenv("WTP_WIRE_MAX_BYTES");
+            const size_t wire_bytes = ((file.size() + kMaxPayload - 1) / kMaxPayload) * WireBuffer::kSlot;
+            try {
+                if (cap && *cap && wire_bytes > size_t(std::strtoull(cap, nullptr, 10)))
+                    throw std::runtime_error("the wire buffer (" + std::to_string(wire_bytes) +
+                                             " B) exceeds WTP_WIRE_MAX_BYTES");
+                built = std::make_unique<WireBuffer>(file);
+            } catch (const std::exception &e) {
+                std::cerr << "wSender: fused build unavailable (" << e.what() << "); using the checksum batch\n";
+                fused = false;
+            }
+        }
+        if (!fused) sums = crc.chunks(file.data(), file.size());
         const uint32_t nchunks = uint32_t(fused ? built->count() : sums.size());
 
         Conn c{udp_socket(), addr_of(a.get("host"), port), log};

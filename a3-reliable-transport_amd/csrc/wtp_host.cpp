@@ -60,6 +60,7 @@ struct Pipe {
     uint32_t *dev_out[2] = {nullptr, nullptr};
     uint8_t *pin_ok[2] = {nullptr, nullptr};
     uint8_t *dev_ok[2] = {nullptr, nullptr};
+    void *view_ok0 = nullptr, *view_out0 = nullptr;  // device views of pin_ok[0] / pin_out[0] (zero-copy verify)
     size_t max_pk = 0;                           // packets per slab (results capacity)
     std::once_flag wire_once;                    // the builder's wire slabs, made on first use
     int wire_rc = WTP_OK;
@@ -89,6 +90,10 @@ int pipe_get(Pipe *&out) {
                 H_HIP(hipHostMalloc(reinterpret_cast<void **>(&p.pin_ok[b]), p.max_pk, hipHostMallocDefault));
                 H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_ok[b]), p.max_pk));
             }
+            // the library's own pinned result buffers never move: look their device views
+            // up once, not per zero-copy call
+            H_HIP(hipHostGetDevicePointer(&p.view_ok0, p.pin_ok[0], 0));
+            H_HIP(hipHostGetDevicePointer(&p.view_out0, p.pin_out[0], 0));
             return WTP_OK;
         };
         p.rc = mk();
@@ -379,13 +384,8 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     if (rc) return rc;
     std::lock_guard<std::mutex> g(P->mu);
     const void *dr = dev_view(h_dgrams), *dl = dev_view(h_recv_len);
-    void *dok = nullptr, *dcrc = nullptr;  // the pipeline's pinned result buffers, device view
     if (dr && dl && n <= P->max_pk && n * stride <= kZeroCopyBytes && zero_copy_enabled()) {
-        dok = dev_view(P->pin_ok[0]);
-        dcrc = dev_view(P->pin_out[0]);
-    }
-    if (dok && dcrc) {
-        rc = host_verify_zero_copy(P, dr, stride, dl, n, dok, dcrc, h_ok, h_crc_out);
+        rc = host_verify_zero_copy(P, dr, stride, dl, n, P->view_ok0, P->view_out0, h_ok, h_crc_out);
     } else {
         // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly
         rc = host_verify_loop(P, static_cast<const uint8_t *>(h_dgrams), dr != nullptr, stride, h_recv_len,

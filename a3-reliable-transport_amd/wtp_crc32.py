@@ -191,7 +191,9 @@ def host_build_data_packets(payloads: np.ndarray, seq0: int = 0, wire_stride: in
     """Every DATA datagram of a host buffer (wtp_host_build_data_packets); wire / wire_len
     may be given (e.g. PinnedBuffer arrays), else numpy arrays are allocated.  Slot bytes
     past each datagram are unspecified."""
-    nb = payloads.nbytes if nbytes is None else nbytes
+    nb = payloads.nbytes if nbytes is None else int(nbytes)
+    if nb < 0 or nb > payloads.nbytes:  # the native builder would read past the buffer
+        raise WtpError(f"nbytes {nb} outside [0, {payloads.nbytes}] (the payload buffer's size)")
     n = (nb + MAX_PAYLOAD - 1) // MAX_PAYLOAD
     if wire is None:
         wire = np.zeros(n * wire_stride, dtype=np.uint8)

@@ -159,6 +159,49 @@ def test_argument_validation_without_device():
     assert L.wtp_host_build_data_packets(C.addressof(out), 4, 0, C.addressof(out), 1471, None) == -1
 
 
+def test_host_build_data_packets_rejects_nbytes_past_the_buffer():
+    """an explicit nbytes larger than the payload buffer (or negative) is
+    refused before the native builder could read past it; no device is touched."""
+    import numpy as np
+
+    import wtp_crc32 as W
+    p = np.zeros(3000, dtype=np.uint8)
+    for bad in (3001, 1 << 40, -1):
+        with pytest.raises(W.WtpError, match="nbytes"):
+            W.host_build_data_packets(p, nbytes=bad)
+
+
 def test_version_string():
     import wtp_crc32 as W
     assert b"gfx950" in W.LIB.wtp_version()
+
+
+def test_cpu_crc32_fast_matches_golden_every_length(golden, tmp_path):
+    """wtp::crc32_fast (slice-by-8, the endpoints' small-batch route under --crc gpu) and
+    the drop-in crc32() (the reference's byte loop) against the reference-generated
+    golden CRC of every length 0..1456, compiled from the shipped header."""
+    import oracle as O
+    src = tmp_path / "t.cpp"
+    src.write_text(r'''
+#include "Crc32.hpp"
+#include <cstdio>
+#include <vector>
+int main(int, char **argv) {
+    std::FILE *f = std::fopen(argv[1], "rb");
+    std::vector<unsigned char> b(1 << 22);
+    const size_t got = std::fread(b.data(), 1, b.size(), f);
+    size_t off = 0;
+    for (size_t L = 0; L <= 1456 && off + L <= got; off += L, ++L)
+        std::printf("%u %u\n", crc32(b.data() + off, L), wtp::crc32_fast(b.data() + off, L));
+}
+''')
+    data = b"".join(O.synth_fill_np(L, start_byte=1000 * L).tobytes() for L in range(1457))
+    (tmp_path / "in.bin").write_bytes(data)
+    exe = str(tmp_path / "t")
+    subprocess.run(["g++", "-O2", "-std=c++20", "-I" + os.path.join(ROOT, "a3-reliable-transport_amd", "cpp", "src", "common"),
+                    "-I" + os.path.join(ROOT, "include"), str(src), "-o", exe], check=True)
+    out = subprocess.run([exe, str(tmp_path / "in.bin")], check=True, capture_output=True, text=True).stdout.split("\n")
+    rows = [tuple(map(int, l.split())) for l in out if l]
+    assert len(rows) == 1457
+    want = golden["per_length"]["crc"]
+    assert [r[0] for r in rows] == want[:1457] and [r[1] for r in rows] == want[:1457]

@@ -87,13 +87,14 @@ class Proxy(threading.Thread):
                 self.held = None
 
 
-def run_transfer(bindir, src, tmp, crc="cpu", proxy=False, window=10, timeout=60):
+def run_transfer(bindir, src, tmp, crc="cpu", proxy=False, window=10, timeout=60, env=None, sender_err=None):
+    env = dict(os.environ, **(env or {}))
     rport = _free_port()
     outdir = os.path.join(tmp, "out")
     os.makedirs(outdir, exist_ok=True)
     rlog, slog = os.path.join(tmp, "receiver.log"), os.path.join(tmp, "sender.log")
     recv = subprocess.Popen([os.path.join(bindir, "wReceiver"), "-p", str(rport), "-w", str(window), "-d", outdir,
-                             "-o", rlog, "--crc", crc, "--once"])
+                             "-o", rlog, "--crc", crc, "--once"], env=env)
     px = None
     try:
         time.sleep(0.2)
@@ -104,8 +105,11 @@ def run_transfer(bindir, src, tmp, crc="cpu", proxy=False, window=10, timeout=60
             px.start()
             target = pport
         s = subprocess.run([os.path.join(bindir, "wSender"), "-h", "127.0.0.1", "-p", str(target), "-w", str(window),
-                            "-i", src, "-o", slog, "--crc", crc], timeout=timeout, capture_output=True, text=True)
+                            "-i", src, "-o", slog, "--crc", crc], timeout=timeout, capture_output=True, text=True,
+                           env=env)
         assert s.returncode == 0, s.stderr
+        if sender_err is not None:
+            sender_err.append(s.stderr)
         recv.wait(timeout=10)
     finally:
         if recv.poll() is None:
@@ -171,18 +175,28 @@ def test_c1_nonseekable_input(binaries, golden, tmp_path):
     assert [f"0x{c:08X}" for c in data_log_checksums(slog)] == golden["files"]["input.txt"]["crc"]
 
 
+# Receiver routes of --crc gpu: window-size batches go to the CPU (crc32_fast) by
+# default; WTP_VERIFY_CPU_MAX_BYTES=0 sends every batch to the device.  Sender routes:
+# the fused device builder by default; WTP_WIRE_MAX_BYTES=1 forces its fallback (the
+# checksum batch + per-send headers).
+GPU_ROUTES = {"default": {}, "verify-on-gpu": {"WTP_VERIFY_CPU_MAX_BYTES": "0"},
+              "sender-fallback": {"WTP_WIRE_MAX_BYTES": "1", "WTP_VERIFY_CPU_MAX_BYTES": "0"}}
+
+
 @pytest.mark.gpu
-def test_c1_loopback_gpu_crc(binaries, golden, tmp_path):
+@pytest.mark.parametrize("route", sorted(GPU_ROUTES))
+def test_c1_loopback_gpu_crc(binaries, golden, tmp_path, route):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    # the sender builds every DATA datagram with the fused device builder
-    # (wtp_host_build_data_packets); the receiver verifies on the device
+    env = GPU_ROUTES[route]
     for name in ("input.txt", "input2.txt", "input3.txt"):
         src = os.path.join(GOLD, name)
         d = tmp_path / name
         d.mkdir()
-        out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu")
+        err = []
+        out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu", env=env, sender_err=err)
+        assert ("fused build unavailable" in err[0]) == (route == "sender-fallback"), err[0]
         assert open(out, "rb").read() == open(src, "rb").read()
         assert [f"0x{c:08X}" for c in data_log_checksums(slog)] == golden["files"][name]["crc"]
         assert [f"0x{c:08X}" for c in data_log_checksums(rlog)] == golden["files"][name]["crc"]
@@ -192,7 +206,7 @@ def test_c1_loopback_gpu_crc(binaries, golden, tmp_path):
     src = str(d / "exact.bin")
     data = O.synth_fill_np(1456 * 7, start_byte=77).tobytes()  # whole chunks only: no short tail
     open(src, "wb").write(data)
-    out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu")
+    out, slog, rlog, _ = run_transfer(binaries, src, str(d), crc="gpu", env=env)
     assert open(out, "rb").read() == data
     assert data_log_checksums(slog) == [O.crc32(data[i * 1456:(i + 1) * 1456]) for i in range(7)]
 
@@ -210,11 +224,12 @@ def test_c1_gpu_verify_drops_corruption(binaries, tmp_path):
     assert px.corrupted > 0
 
 
-def _recv_bench(bindir, crc, batch=256, seconds=1.0, corrupt=100):
+def _recv_bench(bindir, crc, batch=256, seconds=1.0, corrupt=100, env=None):
     import json
     port = _free_port()
     recv = subprocess.Popen([os.path.join(bindir, "wReceiver"), "--bench", str(seconds), "-p", str(port), "--crc", crc,
-                             "--batch", str(batch)], stdout=subprocess.PIPE, text=True)
+                             "--batch", str(batch)], stdout=subprocess.PIPE, text=True,
+                            env=dict(os.environ, **(env or {})))
     try:
         time.sleep(0.3)
         s = subprocess.run([os.path.join(bindir, "wBlast"), "-h", "127.0.0.1", "-p", str(port), "--seconds",
@@ -239,11 +254,19 @@ def test_batched_receive_bench_cpu(binaries):
 
 
 @pytest.mark.gpu
-def test_batched_receive_bench_gpu(binaries):
+@pytest.mark.parametrize("cpu_max", [None, "0"])
+def test_batched_receive_bench_gpu(binaries, cpu_max):
+    """--crc gpu: with the default crossover some batches go to each side; with
+    WTP_VERIFY_CPU_MAX_BYTES=0 every batch is one device call.  Either way exactly the
+    corrupted datagrams fail."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    sent, got = _recv_bench(binaries, "gpu", batch=1024)
+    env = {} if cpu_max is None else {"WTP_VERIFY_CPU_MAX_BYTES": cpu_max}
+    sent, got = _recv_bench(binaries, "gpu", batch=1024, env=env)
     assert got["mode"] == "gpu" and got["datagrams"] > 1000
     bad = got["datagrams"] - got["ok"]
     assert 0.5 * got["datagrams"] / 100 <= bad <= 1.5 * got["datagrams"] / 100 + 2, got
+    if cpu_max == "0":
+        assert got["gpu_batches"] == got["batches"] and got["cpu_verify_max_bytes"] == 0, got
+

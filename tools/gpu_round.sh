@@ -68,6 +68,16 @@ for s in $STEPS; do
              WTP_LIB="$ROOT/$lib" run "ab_$v" 300 python tools/bench_configs.py --only "${CFG_ONLY:-c5}" --out "$OUT/ab_$v.json"
            done ;;
     listavail) run listavail 120 rocprofv3 --list-avail ;;
+    xover) run xover 200 ./tools/bin/verify_crossover 400 ;;
+    tl)    run tl 200 python tools/tl_probe.py --out "$OUT/tl_phases.json"
+           cd /tmp
+           run tlpmc1 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum \
+             TCP_UTCL1_STALL_MULTI_MISS_sum --output-format csv -d "$OUT/tlpmc1" -o tl -- python3 "$ROOT/tools/tl_probe.py"
+           run tlpmc2 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum \
+             TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_THRASHING_STALL_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE \
+             --output-format csv -d "$OUT/tlpmc2" -o tl -- python3 "$ROOT/tools/tl_probe.py"
+           cd "$ROOT"
+           python3 tools/tl_summary.py "$OUT/tl_phases.json" "$OUT/tl_counters.json" $(find "$OUT/tlpmc1" "$OUT/tlpmc2" -name "*counter_collection.csv") > "$OUT/tl_summary.log" 2>&1 || true ;;
     recvsmall) for m in cpu gpu; do for b in ${RECV_BATCHES:-1 10 64}; do
              P=$((20000 + RANDOM % 20000))
              timeout -k 10 60 ./a3-reliable-transport_amd/bin/wReceiver --bench 3 -p $P --crc $m --batch $b \
