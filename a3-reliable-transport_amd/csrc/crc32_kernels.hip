@@ -56,6 +56,9 @@ constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
 #define WTP_PC_S 64
 #endif
 constexpr int kPieceS = WTP_PC_S;
+#ifndef WTP_BR_BLOCKED
+#define WTP_BR_BLOCKED 0  // k_fixed_braid round order (A/B builds: 1 = a contiguous block per workgroup)
+#endif
 static_assert(kPieceS == 64 || kPieceS == 128, "piece size");
 constexpr uint32_t kHinitWords = (kPieceS + 4) & ~3;  // shift(~0, h), h = 0..kPieceS, padded
 constexpr uint32_t kMaxVarLen = 4096;
@@ -487,7 +490,13 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
 
     constexpr uint32_t kFrame = 256u * ROWS;
     const uint64_t rounds = (n + 3) >> 2;
-    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    // Round order.  Shipped: grid-interleaved, wave (b, w) takes rounds b*nwave + w + i*rstep,
+    // so the whole grid moves through the batch as one front.  WTP_BR_BLOCKED=1 (A/B builds,
+    // CRC epilogue only): workgroup b takes a contiguous block of rounds, its waves
+    // interleaved inside it, so each CU walks its own few address translations.
+    constexpr bool kBlocked = WTP_BR_BLOCKED && !BEpi::kFixup && !BEpi::kCopy;
+    const uint64_t rstep = kBlocked ? uint64_t(nwave) : uint64_t(gridDim.x) * nwave;
+    const uint64_t rend = kBlocked ? rounds * (blockIdx.x + 1) / gridDim.x : rounds;  // this wave's last round + 1
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // the advance T past the last row, deferred from the rounds (it commutes with
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
-        const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
+        const bool on = h == 0 && (lane >> 3) < k && rr < rend && p < n;
         epi.put(p, acc, on, pre);
         if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
@@ -605,7 +614,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if (++k == kGroup) flush(rr + rstep, true);
     };
 
-    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
+    uint64_t r = kBlocked ? rounds * blockIdx.x / gridDim.x + wave : uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
@@ -649,28 +658,28 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // builder: only 2 waves per CU, so each wave keeps more bytes in flight)
         Round C;
         load_round(r + rstep, B);
-        while (r < rounds) {
+        while (r < rend) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
             load_round(r + 2 * rstep, C);
             crc_round(r, A);
             r += rstep;
-            if (r >= rounds) break;
+            if (r >= rend) break;
             load_round(r + 2 * rstep, A);
             crc_round(r, B);
             r += rstep;
-            if (r >= rounds) break;
+            if (r >= rend) break;
             load_round(r + 2 * rstep, B);
             crc_round(r, C);
             r += rstep;
         }
     } else {
-        while (r < rounds) {
+        while (r < rend) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
             load_round(r + rstep, B);
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
             r += rstep;
-            if (r >= rounds) break;
+            if (r >= rend) break;
             load_round(r + rstep, A);
             crc_round(r, B);
             r += rstep;
@@ -900,6 +909,52 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
     }
 }
 
+// Span staging by LDS-DMA (WTP_PC_DMA=1): the same slot image as load_span + the
+// ds_write_b128 staging below, written by `buffer_load_dwordx4 ... lds` straight from
+// memory.  An LDS-DMA instruction writes 64 consecutive 16-B positions (wave-uniform base
+// in M0 + 16 * lane), so the per-256-B padding is made on the SOURCE side: position q of
+// the slot holds chunk q - q/17 (the inverse of stage_addr; every 17th position is padding
+// and receives a duplicate chunk that no window reads).  Positions 0..kPcSlotPos-1: four
+// full instructions and 34 lanes of a fifth.  Issued as inline asm, so the compiler keeps
+// no count of them: the loop waits for them itself (vmcnt(0) before the slot is read) and
+// lets the window reads finish (lgkmcnt(0)) before the next span may overwrite the slot.
+#ifndef WTP_PC_DMA
+#define WTP_PC_DMA 1  // 0: register staging (load_span + ds_write_b128), the round-3 form (A/B builds)
+#endif
+constexpr uint32_t kPcSlotPos = kPcSlot / 16;                 // 290 positions of 16 B
+constexpr uint32_t kPcDmaRegs = (kPcSlotPos + 63) / 64;       // 5 instructions
+static_assert(kPcSlotPos - 64 * (kPcDmaRegs - 1) <= 64, "slot positions");
+struct SpanDma {
+    uint32_t coff[kPcDmaRegs];  // per lane: 16 * (source chunk of slot position 64 i + lane)
+    uint32_t slot;              // LDS byte address of the wave's slot (wave-uniform)
+    __device__ __forceinline__ SpanDma(uint32_t slot_addr, uint32_t lane) : slot(slot_addr) {
+#pragma unroll
+        for (uint32_t i = 0; i < kPcDmaRegs; ++i) {
+            const uint32_t q = 64u * i + lane;
+            coff[i] = 16u * (q - q / 17u);
+        }
+    }
+    // the span of 16-B chunks from view offset b16 (16-aligned, may be "negative" or past
+    // the view: those offsets read 0 without touching memory) into the slot
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, int32_t b16, uint32_t lane) const {
+        // lgkmcnt(0) first: this wave's window reads of the slot have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t i = 0; i < kPcDmaRegs; ++i) {
+            const uint32_t voff = uint32_t(b16) + coff[i];
+            const uint32_t m0v = slot + 1024u * i;
+            uint32_t keep;
+            if (i + 1 < kPcDmaRegs || lane < kPcSlotPos - 64u * (kPcDmaRegs - 1))
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep)
+                             : "v"(voff), "s"(rs), "s"(m0v)
+                             : "memory");
+        }
+    }
+    __device__ __forceinline__ static void wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+};
+
 // The wave's packets form one stream of 64-B pieces (each packet cut into pieces counted
 // back from its end, the head piece possibly shorter).  A round takes the next pieces,
 // one per lane, up to 64 and up to the first piece whose window falls outside the span
@@ -911,8 +966,9 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 //      previous round) and assigns lane -> (packet, piece);
 //   2. stages the span into its LDS slot: it was loaded during the previous round (it
 //      starts at most 64 B before that round's last window ends: speculative, exact for
-//      packed and strided batches); a miss loads it now.  All global loads are
-//      lane-contiguous 16-B chunks, 1 KiB per wave instruction;
+//      packed and strided batches); a miss loads it now.  The span goes from memory
+//      straight into the slot by LDS-DMA (SpanDma, 5 instructions of 1 KiB; round 3
+//      loaded it into 20 VGPRs and stored it with 5 ds_write_b128: C5 47.9 -> 46.1 us);
 //   3. reads each lane's 64-B window from the slot and issues the next round's metadata
 //      and span loads;
 //   4. runs the slice-by-4 chain over the window (bytes before the packet masked to
@@ -954,7 +1010,11 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
     uint32_t skip = 0, carry = 0;  // pieces of packet p0 done in earlier rounds, their register
     int32_t spec = kNoSpan;        // view offset of the prefetched span
+#if WTP_PC_DMA
+    const SpanDma dma(__builtin_amdgcn_readfirstlane(uint32_t(uintptr_t(slot))), lane);
+#else
     u32x4 x[kPcSpanRegs];
+#endif
     uint32_t nrounds = 0, done = 0;
     hi = uniform64(hi);  // wave-uniform in SGPRs: the round's packet arithmetic stays scalar
     for (uint64_t p0 = uniform64(lo); p0 < hi;) {
@@ -1014,6 +1074,13 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         // --- stage the span ---------------------------------------------------------------
         const bool hit = __ballot(active && (ws < spec || we - spec > kSpanBytes)) == 0;
         int32_t sbase = spec;
+#if WTP_PC_DMA
+        if (!hit) {
+            dma.issue(rs, lo16, lane);  // the miss pays its latency here
+            sbase = lo16;
+        }
+        SpanDma::wait();  // the slot holds the span (prefetched, or just loaded)
+#else
         if (!hit) {
             load_span(rs, lo16, lane, x);
             sbase = lo16;
@@ -1022,6 +1089,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
         for (uint32_t i = 0; i + 1 < kPcSpanRegs; ++i) *(lu32x4 *)(slot + stage_addr(64u * i + lane)) = x[i];
         if (lane < kPcChunks - 64u * (kPcSpanRegs - 1)) *(lu32x4 *)(slot + stage_addr(64u * (kPcSpanRegs - 1) + lane)) = x[kPcSpanRegs - 1];
+#endif
         __builtin_amdgcn_wave_barrier();
         // the window's five 16-B blocks, aligned (dword-aligned variants without the
         // rotation below were slower on C5: ds_read2_b32 pairs at the 64-B lane stride
@@ -1051,7 +1119,11 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         const uint64_t p0n = p0 + last_pk + (partial ? 0u : 1u);
         meta(p0n);  // first: the next round waits for these, not for the span
         spec = p0n < hi ? ((last_we - kPieceS) & ~15) : kNoSpan;
+#if WTP_PC_DMA
+        if (spec != kNoSpan) dma.issue(rs, spec, lane);  // wave-uniform branch
+#else
         load_span(rs, spec, lane, x);
+#endif
 
         // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
         const uint32_t a = uint32_t(ws) & 15u;
@@ -1251,9 +1323,10 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 // pprobe) define WTP_AB_BUILD to build variants.  A misconfigured product build is a
 // compile error, not a library that runs wrong.
 #ifndef WTP_AB_BUILD
-static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1,
+static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
-static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
+static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0 && WTP_BR_BLOCKED == 0,
+              "product build: no probe / prologue ablation / round-order variant");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");

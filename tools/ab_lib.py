@@ -43,9 +43,13 @@ st = torch.cuda.current_stream()
 sp = st.cuda_stream
 n = a.n
 P = 1456
-if a.what in ("build", "crc", "verify"):
-    pay = torch.empty(n * P + 64, dtype=torch.uint8, device="cuda")
-    L0.wtp_synth_fill(pay.data_ptr(), 0, n * P, 0x5EED, sp)
+if a.what in ("build", "crc", "verify", "crcalt"):
+    # crcalt: two n-packet batches in one 2n buffer, the calls alternate between them (no
+    # launch re-reads what the previous one read: a streaming sender / receiver)
+    halves = 2 if a.what == "crcalt" else 1
+    pay = torch.empty(halves * n * P + 64, dtype=torch.uint8, device="cuda")
+    L0.wtp_synth_fill(pay.data_ptr(), 0, halves * n * P, 0x5EED, sp)
+    ncall = [0]
     wire = torch.empty(n * 1472 + 64, dtype=torch.uint8, device="cuda")
     wl = torch.empty(n, dtype=torch.int32, device="cuda")
     L0.wtp_build_data_packets(pay.data_ptr(), n * P, 0, wire.data_ptr(), 1472, wl.data_ptr(), sp)
@@ -68,6 +72,9 @@ def call(L):
         L.wtp_build_data_packets(pay.data_ptr(), n * P, 0, wire.data_ptr(), 1472, wl.data_ptr(), sp)
     elif a.what == "crc":
         L.wtp_crc32_batch_fixed(pay.data_ptr(), P, P, n, out.data_ptr(), sp)
+    elif a.what == "crcalt":
+        ncall[0] += 1
+        L.wtp_crc32_batch_fixed(pay.data_ptr() + (ncall[0] % 2) * n * P, P, P, n, out.data_ptr(), sp)
     elif a.what == "verify":
         L.wtp_crc32_verify_batch(wire.data_ptr(), 1472, wl.data_ptr(), n, ok.data_ptr(), None, sp)
     elif a.what == "c5":
@@ -91,7 +98,7 @@ for r in range(a.rounds):
         res[p].append(s.elapsed_time(e) / 10 * 1e3)
         if r == 0 and a.what == "build":
             checks[p] = bool(torch.equal(wire, ref_wire))
-        if r == 0 and a.what == "crc":
+        if r == 0 and a.what in ("crc", "crcalt"):
             if "want_crc" not in checks:
                 checks["want_crc"] = out.clone()
             checks[p] = bool(torch.equal(out, checks["want_crc"]))

@@ -34,6 +34,22 @@ for s in $STEPS; do
   case "$s" in
     testsvar) run gpu_tests_var 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "var or packed or zipf or mixed or every_length or smoke" ;;
     testsbuild) run gpu_tests_build 600 python -u -m pytest tests/test_gpu_parity.py tests/test_loopback.py -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "build or loopback or verify_drops or receive_bench" ;;
+    testslib) for t in ${TEST_LIBS}; do
+             WTP_LIB="$ROOT/a3-reliable-transport_amd/lib/ab/$t.so" run "gpu_tests_$t" 600 python -u -m pytest tests -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "${TEST_K:-not loopback and not bench_}"
+           done ;;
+    abcrcalt) run abcrcalt 300 python tools/ab_lib.py --what crcalt --n ${AB_N:-1048576} ${AB_LIBS} ;;
+    abcrc2m) run abcrc2m 300 python tools/ab_lib.py --what crc --n 2097152 ${AB_LIBS} ;;
+    c5sq)  for lib in ${SQ_LIBS:-product}; do
+             if [ "$lib" = product ]; then LP="$ROOT/a3-reliable-transport_amd/lib/libwtp_crc32.so"; else LP="$ROOT/a3-reliable-transport_amd/lib/ab/$lib.so"; fi
+             WTP_LIB="$LP" run "sq_$lib" 400 bash tools/prof_pieces.sh "$TAG/sq_$lib"
+             cd /tmp
+             WTP_LIB="$LP" run "fetch_$lib" 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/sq_$lib/fetch" -o c5 \
+               -- python3 "$ROOT/tools/prof_pieces.py" 3
+             cd "$ROOT"
+           done
+           python3 tools/sq_json.py "$OUT/c5_counters.json" $(for lib in ${SQ_LIBS:-product}; do echo "$lib=$OUT/sq_$lib"; done) > "$OUT/sq_json.log" 2>&1 || true ;;
+    profwin) python3 tools/rocprof_window.py $(find "$OUT/prof" -name "*kernel_trace.csv" | head -1) "k_fixed_braid<6" 20 \
+               "$OUT/rocprof_timed_window.json" $(python3 -c "import json,sys;print([json.loads(l) for l in open('$OUT/prof.log') if l.startswith('{')][-1]['warmup_run'])") > "$OUT/profwin.log" 2>&1 || true ;;
     tests) run gpu_tests 900 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;        # the driver's invocation
     bench2) run bench2 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
