@@ -494,9 +494,15 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // so the whole grid moves through the batch as one front.  WTP_BR_BLOCKED=1 (A/B builds,
     // CRC epilogue only): workgroup b takes a contiguous block of rounds, its waves
     // interleaved inside it, so each CU walks its own few address translations.
+    // WTP_BR_BLOCKED=2: the 8 workgroup classes b % 8 (the XCDs the blocks are dealt to, round
+    // robin; a speed assumption only) each take a contiguous eighth of the rounds, interleaved
+    // over the class's workgroups, so each CU touches the translations of an eighth.
     constexpr bool kBlocked = WTP_BR_BLOCKED && !BEpi::kFixup && !BEpi::kCopy;
-    const uint64_t rstep = kBlocked ? uint64_t(nwave) : uint64_t(gridDim.x) * nwave;
-    const uint64_t rend = kBlocked ? rounds * (blockIdx.x + 1) / gridDim.x : rounds;  // this wave's last round + 1
+    const bool xblk = kBlocked && WTP_BR_BLOCKED == 2 && (gridDim.x & 7u) == 0;
+    const uint32_t xcls = blockIdx.x & 7u, xslot = blockIdx.x >> 3, xper = gridDim.x >> 3;
+    const uint64_t rstep = !kBlocked ? uint64_t(gridDim.x) * nwave : (xblk ? uint64_t(xper) * nwave : uint64_t(nwave));
+    const uint64_t rend = !kBlocked ? rounds
+                          : (xblk ? rounds * (xcls + 1) / 8 : rounds * (blockIdx.x + 1) / gridDim.x);  // this wave's last round + 1
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -614,7 +620,8 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if (++k == kGroup) flush(rr + rstep, true);
     };
 
-    uint64_t r = kBlocked ? rounds * blockIdx.x / gridDim.x + wave : uint64_t(blockIdx.x) * nwave + wave;
+    uint64_t r = !kBlocked ? uint64_t(blockIdx.x) * nwave + wave
+                 : (xblk ? rounds * xcls / 8 + uint64_t(xslot) * nwave + wave : rounds * blockIdx.x / gridDim.x + wave);
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out

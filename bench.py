@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the CRC kernel leaves free (wtp_reserve_cus); default 8 with the gather "
                          "(for the overlapped RCCL gather's workgroups), else 0")
+    ap.add_argument("--gather-every", type=int, default=1,
+                    help="with the gather: gather the results of this many steps in one collective (the step's "
+                         "stream-event hops are paid once per group)")
     ap.add_argument("--gather-n1", action="store_true",
                     help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box streaming-read probe")
@@ -369,50 +372,83 @@ def init_one_rank_group(local: int) -> None:
 
 
 class Pipe:
-    """Step i: the CRC of this rank's shard into outs[i % 2] on `stream`, then (with the
-    gather) the RCCL gather of those results to rank 0, asynchronous: it runs on the
+    """Step i: the CRC of this rank's shard into a result slot on `stream`, then (with the
+    gather) the RCCL gather of the results to rank 0, asynchronous: it runs on the
     collective's stream, on the CUs the CRC kernel leaves free (wtp_reserve_cus), while
-    step i+1's CRC runs; outs[b] is rewritten only after its gather is done.  `bufs` may
-    hold several shards of equal size: step i reads bufs[i % len(bufs)] (the alternating-
-    buffer leg)."""
+    the next steps' CRCs run.  Result slots come in two groups of `every` slots; a group is
+    gathered in one collective when it is full (every = 1: each step's results right
+    after its launch), and rewritten only after that gather is done.  `bufs` may hold
+    several shards of equal size: step i reads bufs[i % len(bufs)] (the alternating-buffer
+    leg)."""
 
-    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev):
+    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1):
         import torch
         self.W, self.shard, self.bufs, self.n, self.stream = W, shard, bufs, n, stream
         self.do_gather, self.world, self.rank, self.gathered = do_gather, world, rank, gathered
-        self.outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2 if do_gather else 1)]
-        self.works = [None] * len(self.outs)
-        self.i = 0
+        self.K = max(1, int(every)) if do_gather else 1
+        self.groups = [torch.empty(self.K * n, dtype=torch.int32, device=dev) for _ in range(2 if do_gather else 1)]
+        self.works = [None] * len(self.groups)
+        self.i = 0       # steps launched
+        self.pos = 0     # result slots used (a flush skips to the next group)
+        self.last_m = 0  # slots in the last gather
+        self.last_pos = 0
+
+    def _group(self, pos):
+        return (pos // self.K) % len(self.groups)
 
     def wait_slot(self):
-        b = self.i % len(self.outs)
-        if self.works[b] is not None:
-            self.works[b].wait()
-            self.works[b] = None
+        if self.pos % self.K == 0:  # first slot of a group: its previous gather must be done
+            g = self._group(self.pos)
+            if self.works[g] is not None:
+                self.works[g].wait()
+                self.works[g] = None
 
     def launch(self):
-        self.W.crc32_batch_fixed(self.bufs[self.i % len(self.bufs)], PAYLOAD, PAYLOAD, self.n,
-                                 self.outs[self.i % len(self.outs)], self.stream)
+        k = self.pos % self.K
+        out = self.groups[self._group(self.pos)][k * self.n:(k + 1) * self.n]
+        self.W.crc32_batch_fixed(self.bufs[self.i % len(self.bufs)], PAYLOAD, PAYLOAD, self.n, out, self.stream)
+        self.last_pos = self.pos
+
+    def _gather(self, m):
+        g = self._group(self.pos - 1)
+        out = self.gathered[:self.world * m * self.n] if self.gathered is not None else None
+        self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
+        self.last_m = m
 
     def finish(self):
-        if self.do_gather:
-            b = self.i % 2
-            self.works[b] = self.shard.gather_crcs_async(self.outs[b], self.world, self.rank, out=self.gathered)
         self.i += 1
+        self.pos += 1
+        if self.do_gather and self.pos % self.K == 0:
+            self._gather(self.K)
 
     def step(self):
         self.wait_slot()
         self.launch()
         self.finish()
 
+    def flush(self):
+        """Gather a partly filled group (the end of a timed region), then start a new group."""
+        m = self.pos % self.K
+        if self.do_gather and m:
+            self._gather(m)
+            self.pos += self.K - m
+
     def drain(self):
+        self.flush()
         for b, w in enumerate(self.works):
             if w is not None:
                 w.wait()
                 self.works[b] = None
 
     def last_out(self):
-        return self.outs[(self.i - 1) % len(self.outs)]
+        g, k = self._group(self.last_pos), self.last_pos % self.K
+        return self.groups[g][k * self.n:(k + 1) * self.n]
+
+    def gathered_vector(self):
+        """Rank 0 after drain(): the gathered u32 results of the last step of every rank, in
+        rank order (each rank's block of the last gather holds last_m result vectors)."""
+        m = self.last_m
+        return self.gathered[:self.world * m * self.n].view(self.world, m * self.n)[:, (m - 1) * self.n:].reshape(-1)
 
 
 def time_steps(pipe: Pipe, steps: int, world: int):
@@ -434,7 +470,7 @@ def time_steps(pipe: Pipe, steps: int, world: int):
         pipe.launch()
         ends[i].record(pipe.stream)
         pipe.finish()
-    pipe.drain()
+    pipe.drain()  # gathers a partly filled group, waits for every gather
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -450,7 +486,7 @@ def kstats(kern: list, nbytes: int) -> dict:
             "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4_PACKETS // 8) -> dict:
+def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4_PACKETS // 8, every: int = 1) -> dict:
     """Equal-work reference for the N > 1 lines, in the N = 1 process: rank 0's C4 shard
     (2 M x 1456 B = 3.05 GB, the first 2 M packets of the global stream) through the SAME
     pipelined step the N > 1 ranks run (own stream, 8 reserved CUs, the asynchronous RCCL
@@ -472,14 +508,14 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
     torch.cuda.set_stream(stream)
     W.reserve_cus(8, torch.cuda.current_device())
     try:
-        gathered = torch.empty(n, dtype=torch.int32, device=dev)
-        pipe = Pipe(W, shard, [buf], n, stream, True, 1, 0, gathered, dev)
+        gathered = torch.empty(every * n, dtype=torch.int32, device=dev)
+        pipe = Pipe(W, shard, [buf], n, stream, True, 1, 0, gathered, dev, every=every)
         settle(pipe.step, stream, warmup)
         pipe.drain()
         torch.cuda.synchronize()
         kern, el = time_steps(pipe, steps, 1)
         import numpy as np
-        par = parity_digest(gathered.cpu().numpy().view(np.uint32))
+        par = parity_digest(pipe.gathered_vector().cpu().numpy().view(np.uint32))
     finally:
         W.reserve_cus(0, torch.cuda.current_device())
         torch.cuda.set_stream(prev)
@@ -488,6 +524,7 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
     out = {"what": "rank 0's C4 shard (2 M x 1456 B) through the N > 1 step on this GPU: own stream, "
                    "8 reserved CUs, asynchronous one-rank RCCL gather of the u32 results",
            "packets": n, "bytes_per_launch": nbytes, "steps": steps,
+           "gather_every": pipe.K,
            "step_ms": round(el / steps * 1e3, 4), "value_GiBs": round(nbytes * steps / el / 2**30, 2),
            "parity_match": par["match"], "sha256": par["sha256"]}
     out.update(kstats(kern, nbytes))
@@ -561,9 +598,10 @@ def main():
     reserve = args.reserve_cus if args.reserve_cus is not None else (8 if do_gather else 0)
     if reserve:
         W.reserve_cus(reserve, torch.cuda.current_device())
-    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
-    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev)
-    out = pipe.outs[0]
+    every = args.gather_every if do_gather else 1
+    gathered = torch.empty(world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
+    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every)
+    out = torch.empty(n, dtype=torch.int32, device=dev)  # the read-probe leg's CRC launches
 
     def crc():
         W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
@@ -590,7 +628,7 @@ def main():
     parity = None
     if rank == 0:
         import numpy as np
-        vec = (gathered if gathered is not None else pipe.last_out()).cpu().numpy().view(np.uint32)
+        vec = (pipe.gathered_vector() if gathered is not None else pipe.last_out()).cpu().numpy().view(np.uint32)
         parity = parity_digest(vec)
         if parity["match"] is None:  # no reference digest for this size: oracle spot check
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -623,6 +661,7 @@ def main():
                    "packets_per_rank": n, "payload_bytes": PAYLOAD, "global_packets": n * world,
                    "parallelism": f"packet shards x{world}" if world > 1 else "single GPU",
                    "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
+                   "gather_every": every if do_gather else None,
                    "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,
@@ -650,7 +689,7 @@ def main():
         # after the timed region and the probe: neither leg touches the headline numbers
         line["alt_buffer"] = alt_buffer_leg(W, buf, nbytes, n, dev, stream, args.steps, args.warmup)
         line["alt_buffer_kernel_ms"] = line["alt_buffer"]["kernel_ms_mean"]
-        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup)
+        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup, every=args.gather_every)
         if line["c4_shard_1gpu"]["parity_match"] is False:
             parity["c4_shard_1gpu"] = False
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -132,7 +132,8 @@ def _no_gpu(monkeypatch, bench):
     monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
 
 
-def test_n1_extra_legs_fields_on_cpu(monkeypatch):
+@pytest.mark.parametrize("every", [1, 3])
+def test_n1_extra_legs_fields_on_cpu(monkeypatch, every):
     """The two legs the N = 1 line carries after its timed region: alt_buffer (two 1 M
     buffers in turn) and c4_shard_1gpu (the N > 1 pipelined step with a one-rank gather,
     here over gloo): fields, sizes, the CU reservation restored, and the gathered vector
@@ -160,10 +161,11 @@ def test_n1_extra_legs_fields_on_cpu(monkeypatch):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
     try:
         W.launches = 0
-        c4 = bench.c4_shard_leg(W, shard, "cpu", 0, steps=4, warmup=5, n=n)
+        c4 = bench.c4_shard_leg(W, shard, "cpu", 0, steps=4, warmup=5, n=n, every=every)
     finally:
         dist.destroy_process_group()
     assert c4["packets"] == n and c4["bytes_per_launch"] == nbytes and c4["steps"] == 4
+    assert c4["gather_every"] == every  # every = 3 over 4 steps: one full group, one partial
     assert W.reserved == [8, 0]  # 8 CUs for the gather while the leg runs, then restored
     assert W.launches == 3 + 4  # settle + the timed steps, one launch each
     want = O.batch_fixed(O.synth_fill_np(nbytes), bench.PAYLOAD, bench.PAYLOAD, n)

@@ -59,6 +59,16 @@ for s in $STEPS; do
     prof)  cd /tmp && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
            cd "$ROOT" ;;
+    profnox) cd /tmp && run profnox 400 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/profnox" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extras
+           cd "$ROOT" ;;
+    pmcnew) cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-probe --no-extras
+           cd "$ROOT"
+           python3 tools/pmc_traffic.py $(find "$OUT/pmc" -name "*counter_collection.csv" | head -1) "$OUT/pmc_traffic.json" 1048576 > "$OUT/pmc_traffic.log" 2>&1 || true ;;
+    gev)   for k in ${GEV:-1 2 4}; do
+             run "c4gather_k$k" 300 python bench.py --steps 20 --warmup 5 --gather-n1 --packets-per-rank 2097152 --gather-every $k --no-cpu-baseline --no-probe
+           done ;;
     transient) run transient 200 python -u tools/transient.py --out "$OUT/transient.json" ;;
     pmc)   cd /tmp && run pmc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
              -d "$OUT/pmc" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-probe
