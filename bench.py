@@ -62,9 +62,10 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the CRC kernel leaves free (wtp_reserve_cus); default 8 with the gather "
                          "(for the overlapped RCCL gather's workgroups), else 0")
-    ap.add_argument("--gather-every", type=int, default=1,
+    ap.add_argument("--gather-every", type=int, default=2,
                     help="with the gather: gather the results of this many steps in one collective (the step's "
-                         "stream-event hops are paid once per group)")
+                         "stream-event hops are paid once per group; 2: 0.480 -> 0.468 ms per C4 step, "
+                         "profiles/r04e)")
     ap.add_argument("--gather-n1", action="store_true",
                     help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box streaming-read probe")
@@ -379,7 +380,7 @@ class Pipe:
     gathered in one collective when it is full (every = 1: each step's results right
     after its launch), and rewritten only after that gather is done.  `bufs` may hold
     several shards of equal size: step i reads bufs[i % len(bufs)] (the alternating-buffer
-    leg)."""
+    leg).  `gathered` (rank 0) holds 2 x world x every x n results: one half per group."""
 
     def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1):
         import torch
@@ -390,7 +391,7 @@ class Pipe:
         self.works = [None] * len(self.groups)
         self.i = 0       # steps launched
         self.pos = 0     # result slots used (a flush skips to the next group)
-        self.last_m = 0  # slots in the last gather
+        self.last_m, self.last_g = 0, 0  # slots and group of the last gather
         self.last_pos = 0
 
     def _group(self, pos):
@@ -410,10 +411,15 @@ class Pipe:
         self.last_pos = self.pos
 
     def _gather(self, m):
+        # each group gathers into its own half of `gathered`: two gathers may be in flight
+        # at once, and a process group need not complete them in order (gloo does not)
         g = self._group(self.pos - 1)
-        out = self.gathered[:self.world * m * self.n] if self.gathered is not None else None
+        out = None
+        if self.gathered is not None:
+            half = self.world * self.K * self.n
+            out = self.gathered[g * half:g * half + self.world * m * self.n]
         self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
-        self.last_m = m
+        self.last_m, self.last_g = m, g
 
     def finish(self):
         self.i += 1
@@ -447,8 +453,9 @@ class Pipe:
     def gathered_vector(self):
         """Rank 0 after drain(): the gathered u32 results of the last step of every rank, in
         rank order (each rank's block of the last gather holds last_m result vectors)."""
-        m = self.last_m
-        return self.gathered[:self.world * m * self.n].view(self.world, m * self.n)[:, (m - 1) * self.n:].reshape(-1)
+        m, half = self.last_m, self.world * self.K * self.n
+        g = self.gathered[self.last_g * half:self.last_g * half + self.world * m * self.n]
+        return g.view(self.world, m * self.n)[:, (m - 1) * self.n:].reshape(-1)
 
 
 def time_steps(pipe: Pipe, steps: int, world: int):
@@ -508,7 +515,7 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
     torch.cuda.set_stream(stream)
     W.reserve_cus(8, torch.cuda.current_device())
     try:
-        gathered = torch.empty(every * n, dtype=torch.int32, device=dev)
+        gathered = torch.empty(2 * every * n, dtype=torch.int32, device=dev)
         pipe = Pipe(W, shard, [buf], n, stream, True, 1, 0, gathered, dev, every=every)
         settle(pipe.step, stream, warmup)
         pipe.drain()
@@ -599,7 +606,7 @@ def main():
     if reserve:
         W.reserve_cus(reserve, torch.cuda.current_device())
     every = args.gather_every if do_gather else 1
-    gathered = torch.empty(world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
+    gathered = torch.empty(2 * world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
     pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every)
     out = torch.empty(n, dtype=torch.int32, device=dev)  # the read-probe leg's CRC launches
 

@@ -223,3 +223,65 @@ def test_gather_async_requires_out_on_dst():
         shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=None)
     with pytest.raises(ValueError):
         shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=torch.zeros(7, dtype=torch.int32))
+
+
+def _bench_pipe_worker(rank, world, port, every, steps, q):
+    """bench.py's own Pipe (results gathered in groups of `every` steps, two groups in
+    flight, a partial group flushed at the end) over gloo, with a stand-in launch that
+    writes rank * 1000 + step * 7 + lane into the step's result slot."""
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd")):
+        sys.path.insert(0, p)
+    import bench
+    import shard as S
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 257
+
+    class FakeW:
+        calls = 0
+
+        def crc32_batch_fixed(self, buf, stride, length, nn, out, stream=None):
+            out.copy_(torch.arange(nn, dtype=torch.int32) + rank * 1000 + FakeW.calls * 7)
+            FakeW.calls += 1
+
+    gathered = torch.empty(2 * world * every * n, dtype=torch.int32) if rank == 0 else None
+    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every)
+    seen = []
+    real = S.gather_crcs_async
+
+    def spy(local, w, r, out=None, **kw):
+        seen.append(local.numel() // n)
+        return real(local, w, r, out=out, **kw)
+
+    S.gather_crcs_async = spy
+    for _ in range(steps):
+        pipe.step()
+    pipe.drain()
+    if rank == 0:
+        q.put((pipe.gathered_vector().numpy().copy(), seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,every,steps", [(2, 1, 3), (2, 2, 5), (3, 4, 6)])
+def test_bench_pipe_grouped_gather(world, every, steps):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_pipe_worker, args=(r, world, port, every, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, seen = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = 257
+    want = np.concatenate([np.arange(n) + r * 1000 + (steps - 1) * 7 for r in range(world)]).astype(np.uint32)
+    assert np.array_equal(got.view(np.uint32), want)
+    # full groups of `every` results, then the partial group the drain flushes
+    assert seen == [every] * (steps // every) + ([steps % every] if steps % every else [])
