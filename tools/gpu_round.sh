@@ -94,6 +94,7 @@ for s in $STEPS; do
              WTP_LIB="$ROOT/$lib" run "ab_$v" 300 python tools/bench_configs.py --only "${CFG_ONLY:-c5}" --out "$OUT/ab_$v.json"
            done ;;
     listavail) run listavail 120 rocprofv3 --list-avail ;;
+    contig) run contig 300 python tools/contig_probe.py --out "$OUT/contig.json" ;;
     xover) run xover 200 ./tools/bin/verify_crossover 400 ;;
     tl)    run tl 200 python tools/tl_probe.py --out "$OUT/tl_phases.json"
            cd /tmp
