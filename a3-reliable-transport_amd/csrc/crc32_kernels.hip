@@ -56,12 +56,6 @@ constexpr uint32_t kBraidBlock = 4 * kBraids;  // one row = 256 bytes
 #define WTP_PC_S 64
 #endif
 constexpr int kPieceS = WTP_PC_S;
-#ifndef WTP_BR_BLOCKED
-#define WTP_BR_BLOCKED 0  // k_fixed_braid round order (A/B builds: 1 = a contiguous block per workgroup)
-#endif
-#ifndef WTP_BR_TLPF
-#define WTP_BR_TLPF 0  // k_fixed_braid<CrcBEpi>: a translation-prefetch wave this many iterations ahead (A/B builds)
-#endif
 static_assert(kPieceS == 64 || kPieceS == 128, "piece size");
 constexpr uint32_t kHinitWords = (kPieceS + 4) & ~3;  // shift(~0, h), h = 0..kPieceS, padded
 constexpr uint32_t kMaxVarLen = 4096;
@@ -486,31 +480,19 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     PC_PROBE(0, __builtin_amdgcn_s_memrealtime());
-    // WTP_BR_TLPF (A/B builds): the workgroup's last wave hashes nothing; it walks the
-    // address translations of the rounds its CU will read WTP_BR_TLPF iterations ahead
-    // of wave 0 (one 4-B LDS-DMA load per iteration into its own unused transposition
-    // slot), so the data waves find them in the CU's UTCL1.
-    constexpr bool kTlpf = WTP_BR_TLPF > 0 && !BEpi::kFixup && !BEpi::kCopy;
-    const uint32_t nwave = kTlpf ? (blockDim.x >> 6) - 1u : blockDim.x >> 6;
+    const uint32_t nwave = blockDim.x >> 6;
     const uint32_t j = lane & (kG - 1);  // braid group (column) within the packet
     const uint32_t q = lane >> 4;        // packet slot within the wave (0..3)
     const StagKeys K(lane);
 
     constexpr uint32_t kFrame = 256u * ROWS;
     const uint64_t rounds = (n + 3) >> 2;
-    // Round order.  Shipped: grid-interleaved, wave (b, w) takes rounds b*nwave + w + i*rstep,
-    // so the whole grid moves through the batch as one front.  WTP_BR_BLOCKED=1 (A/B builds,
-    // CRC epilogue only): workgroup b takes a contiguous block of rounds, its waves
-    // interleaved inside it, so each CU walks its own few address translations.
-    // WTP_BR_BLOCKED=2: the 8 workgroup classes b % 8 (the XCDs the blocks are dealt to, round
-    // robin; a speed assumption only) each take a contiguous eighth of the rounds, interleaved
-    // over the class's workgroups, so each CU touches the translations of an eighth.
-    constexpr bool kBlocked = WTP_BR_BLOCKED && !BEpi::kFixup && !BEpi::kCopy;
-    const bool xblk = kBlocked && WTP_BR_BLOCKED == 2 && (gridDim.x & 7u) == 0;
-    const uint32_t xcls = blockIdx.x & 7u, xslot = blockIdx.x >> 3, xper = gridDim.x >> 3;
-    const uint64_t rstep = !kBlocked ? uint64_t(gridDim.x) * nwave : (xblk ? uint64_t(xper) * nwave : uint64_t(nwave));
-    const uint64_t rend = !kBlocked ? rounds
-                          : (xblk ? rounds * (xcls + 1) / 8 : rounds * (blockIdx.x + 1) / gridDim.x);  // this wave's last round + 1
+    // Round order: grid-interleaved, wave (b, w) takes rounds b*nwave + w + i*rstep, so the
+    // whole grid moves through the batch as one front.  (A contiguous block of rounds per
+    // workgroup, and one per XCD class b % 8, were built in round 4 and measured slower at
+    // every size, DESIGN 7.10, as was a translation-prefetch wave; code in git history,
+    // commits f56e6d4 and 8c994a0.)
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -579,7 +561,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // the advance T past the last row, deferred from the rounds (it commutes with
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
-        const bool on = h == 0 && (lane >> 3) < k && rr < rend && p < n;
+        const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
         epi.put(p, acc, on, pre);
         if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
@@ -628,8 +610,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if (++k == kGroup) flush(rr + rstep, true);
     };
 
-    uint64_t r = !kBlocked ? uint64_t(blockIdx.x) * nwave + wave
-                 : (xblk ? rounds * xcls / 8 + uint64_t(xslot) * nwave + wave : rounds * blockIdx.x / gridDim.x + wave);
+    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
@@ -640,59 +621,24 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
                              {gtab + OFF_INV + 5 * 1024, 65536u + 128u}};
     constexpr int kT = BEpi::kThreads;  // the launcher's workgroup size
     StagFill<4, kT> fill;
-    const bool batched = kTlpf ? nwave * 64u == kT : blockDim.x == kT;  // other sizes: tools/kbench.hip A/B builds
+    const bool batched = blockDim.x == kT;  // other sizes: tools/kbench.hip A/B builds
 #ifndef WTP_BR_PROLOGUE_DIAG  // probe builds only: 1 = no table loads, 2 = no table fill at all
 #define WTP_BR_PROLOGUE_DIAG 0
 #endif
-    const bool data_wave = !kTlpf || wave < nwave;
-    typedef __attribute__((address_space(3))) uint32_t lu32p;
-    lu32p *const tl_prog = (lu32p *)(lds + kBraidXpose + (nwave + 1u) * 2048u);  // wave 0's iteration (TLPF)
-    if (data_wave) {
-        if (batched && WTP_BR_PROLOGUE_DIAG == 0) fill.load(sets);
-        if (WTP_BR_PROLOGUE_DIAG == 1)
-            for (int kk = 0; kk < fill.PER; ++kk) fill.v[kk] = threadIdx.x + kk;
-        epi.pre(group_packet(r), pre);
-        load_round(r, A);
-        PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
-        if (WTP_BR_PROLOGUE_DIAG == 2) {
-        } else if (batched) {
-            fill.store(lds, sets);
-        } else {
-            for (int q2 = 0; q2 < 4; ++q2) fill_stag(lds, sets[q2].off >> 16, (sets[q2].off >> 7) & 1u, sets[q2].g);
-        }
-        if (kTlpf && wave == 0 && lane == 0) *tl_prog = 0u;
+    if (batched && WTP_BR_PROLOGUE_DIAG == 0) fill.load(sets);
+    if (WTP_BR_PROLOGUE_DIAG == 1)
+        for (int kk = 0; kk < fill.PER; ++kk) fill.v[kk] = threadIdx.x + kk;
+    epi.pre(group_packet(r), pre);
+    load_round(r, A);
+    PC_PROBE(1, __builtin_amdgcn_s_memrealtime());
+    if (WTP_BR_PROLOGUE_DIAG == 2) {
+    } else if (batched) {
+        fill.store(lds, sets);
+    } else {
+        for (int q2 = 0; q2 < 4; ++q2) fill_stag(lds, sets[q2].off >> 16, (sets[q2].off >> 7) & 1u, sets[q2].g);
     }
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
     __syncthreads();
-    if constexpr (kTlpf) {
-        if (!data_wave) {
-            const uint32_t scratch = __builtin_amdgcn_readfirstlane(
-                uint32_t(uintptr_t((lchar *)(lds + kBraidXpose + nwave * 2048u))));
-            const uint64_t r0 = uint64_t(blockIdx.x) * nwave;  // wave 0's first round
-            uint64_t it = 0;                                    // iterations walked
-            for (;;) {
-                const uint32_t cur = __hip_atomic_load(tl_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (cur == 0xFFFFFFFFu) break;
-                for (; it <= uint64_t(cur) + WTP_BR_TLPF; ++it) {
-                    const uint64_t rr = r0 + it * rstep;
-                    if (rr >= rounds) break;
-                    const __amdgpu_buffer_rsrc_t rs1 = make_rsrc((const void *)(gbase + rr * 4 * stride), 4u);
-                    uint32_t keep;
-                    const uint32_t zero = 0;
-                    if (lane == 0)
-                        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
-                                     "s_mov_b32 m0, %0"
-                                     : "=&s"(keep)
-                                     : "v"(zero), "s"(rs1), "s"(scratch)
-                                     : "memory");
-                }
-                if (r0 + it * rstep >= rounds) break;
-                __builtin_amdgcn_s_sleep(16);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-    }
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
 
     // 2-way unrolled: one round in flight while the previous one is hashed, no register
@@ -708,37 +654,33 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // builder: only 2 waves per CU, so each wave keeps more bytes in flight)
         Round C;
         load_round(r + rstep, B);
-        while (r < rend) {
+        while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
             load_round(r + 2 * rstep, C);
             crc_round(r, A);
             r += rstep;
-            if (r >= rend) break;
+            if (r >= rounds) break;
             load_round(r + 2 * rstep, A);
             crc_round(r, B);
             r += rstep;
-            if (r >= rend) break;
+            if (r >= rounds) break;
             load_round(r + 2 * rstep, B);
             crc_round(r, C);
             r += rstep;
         }
     } else {
-        uint32_t tl_it = 0;
-        while (r < rend) {
+        while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
-            if (kTlpf && wave == 0 && lane == 0) *tl_prog = tl_it;
-            tl_it += 2;
             load_round(r + rstep, B);
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
             r += rstep;
-            if (r >= rend) break;
+            if (r >= rounds) break;
             load_round(r + rstep, A);
             crc_round(r, B);
             r += rstep;
         }
     }
-    if (kTlpf && wave == 0 && lane == 0) *tl_prog = 0xFFFFFFFFu;
     if (k) flush(0, false);
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);
@@ -1379,8 +1321,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 #ifndef WTP_AB_BUILD
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
-static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0 && WTP_BR_BLOCKED == 0 && WTP_BR_TLPF == 0,
-              "product build: no probe / prologue ablation / round-order variant");
+static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");
@@ -2031,7 +1972,6 @@ template <class BEpi>
 int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
                        hipStream_t st) {
     const int rows = int((len + 255) / 256);
-    constexpr bool kTlpf = WTP_BR_TLPF > 0 && !BEpi::kFixup && !BEpi::kCopy;
     const unsigned threads = BEpi::kThreads;
     const uint64_t rounds = (n + 3) / 4;
     const uint64_t want = (rounds + threads / 64 - 1) / (threads / 64);
@@ -2046,12 +1986,12 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
     const unsigned grid = unsigned(want < cap ? want : cap);
     epi.cinit = init_const(len);
     switch (rows) {
-        case 1: launch_braid_rows<1>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
-        case 2: launch_braid_rows<2>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
-        case 3: launch_braid_rows<3>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
-        case 4: launch_braid_rows<4>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
-        case 5: launch_braid_rows<5>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
-        case 6: launch_braid_rows<6>(grid, threads + (kTlpf ? 64u : 0u), st, base, stride, len, n, epi, s.tabs); break;
+        case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 2: launch_braid_rows<2>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 3: launch_braid_rows<3>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 4: launch_braid_rows<4>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 5: launch_braid_rows<5>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 6: launch_braid_rows<6>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
         default: return fail(WTP_EINVAL, "braid rows %d", rows);
     }
     return launch_check("k_fixed_braid");
