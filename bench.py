@@ -563,6 +563,23 @@ def alt_buffer_leg(W, buf, nbytes: int, n: int, dev, stream, steps: int, warmup:
     return out
 
 
+def run_extra_legs(line: dict, parity: dict, W, shard, buf, nbytes: int, n: int, dev, local: int, stream, args) -> None:
+    """The N = 1 line's alt_buffer and c4_shard_1gpu legs.  A leg that cannot run (e.g. no
+    RCCL on the box) is reported in the line instead of failing the run; a leg whose
+    results differ from the reference's digest marks the parity as failed."""
+    try:
+        line["alt_buffer"] = alt_buffer_leg(W, buf, nbytes, n, dev, stream, args.steps, args.warmup)
+        line["alt_buffer_kernel_ms"] = line["alt_buffer"]["kernel_ms_mean"]
+    except (RuntimeError, OSError) as e:  # WtpError is a RuntimeError
+        line["alt_buffer"] = {"error": f"{e.__class__.__name__}: {e}"[:300]}
+    try:
+        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup, every=args.gather_every)
+        if line["c4_shard_1gpu"]["parity_match"] is False:
+            parity["c4_shard_1gpu"] = False
+    except (RuntimeError, OSError) as e:
+        line["c4_shard_1gpu"] = {"error": f"{e.__class__.__name__}: {e}"[:300]}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -692,13 +709,8 @@ def main():
         line["kernel_ms_max_over_ranks"] = max(per_rank)
         line["step_ms"] = round(el / args.steps * 1e3, 4)
     extras = rank == 0 and world == 1 and not args.gather_n1 and n == 1 << 20 and not args.no_extras
-    if extras:
-        # after the timed region and the probe: neither leg touches the headline numbers
-        line["alt_buffer"] = alt_buffer_leg(W, buf, nbytes, n, dev, stream, args.steps, args.warmup)
-        line["alt_buffer_kernel_ms"] = line["alt_buffer"]["kernel_ms_mean"]
-        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup, every=args.gather_every)
-        if line["c4_shard_1gpu"]["parity_match"] is False:
-            parity["c4_shard_1gpu"] = False
+    if extras:  # after the timed region and the probe: neither leg touches the headline numbers
+        run_extra_legs(line, parity, W, shard, buf, nbytes, n, dev, local, stream, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         hc = host_cores()
         threads = args.cpu_threads or hc["threads"]

@@ -200,3 +200,31 @@ def test_traffic_null_unless_kernel_code_matches(tmp_path):
     assert v is None and info["status"].startswith("stale"), info
     v, info = bench.pmc_traffic(2 << 20, W.LIB_PATH)
     assert v is None
+
+
+def test_extra_leg_failure_is_reported_not_fatal(monkeypatch):
+    """A leg that cannot run (here the C4 leg's RCCL init raises) is recorded in the line
+    and the other leg still runs; a leg with a wrong result vector fails the parity."""
+    from types import SimpleNamespace
+
+    import bench
+    calls = []
+
+    def alt(*a, **k):
+        calls.append("alt")
+        return {"kernel_ms_mean": 0.2}
+
+    def c4_fail(*a, **k):
+        raise RuntimeError("ProcessGroupNCCL is only supported with GPUs")
+
+    monkeypatch.setattr(bench, "alt_buffer_leg", alt)
+    monkeypatch.setattr(bench, "c4_shard_leg", c4_fail)
+    args = SimpleNamespace(steps=3, warmup=1, gather_every=2)
+    line, parity = {}, {"match": True}
+    bench.run_extra_legs(line, parity, None, None, None, 0, 0, "cpu", 0, None, args)
+    assert calls == ["alt"] and line["alt_buffer_kernel_ms"] == 0.2
+    assert "RCCL" in line["c4_shard_1gpu"]["error"] or "NCCL" in line["c4_shard_1gpu"]["error"]
+    assert parity == {"match": True}
+    monkeypatch.setattr(bench, "c4_shard_leg", lambda *a, **k: {"parity_match": False})
+    bench.run_extra_legs(line, parity, None, None, None, 0, 0, "cpu", 0, None, args)
+    assert parity["c4_shard_1gpu"] is False
