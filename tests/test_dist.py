@@ -87,7 +87,7 @@ def run_ranks(world, n_total, use_gpu=False):
     return got
 
 
-@pytest.mark.parametrize("world,n_total", [(2, 1024), (4, 2048), (3, 1001), (4, 4099)])
+@pytest.mark.parametrize("world,n_total", [(2, 1024), (4, 2048), (3, 1001), (4, 4099), (8, 8 * 2048 + 5)])
 def test_gather_matches_single_process(world, n_total):
     """Equal shards (fast gather) and ragged block partitions (n % world != 0: padded
     gather through gather_crcs_var) both return the single-process vector."""
@@ -267,7 +267,7 @@ def _bench_pipe_worker(rank, world, port, every, steps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,every,steps", [(2, 1, 3), (2, 2, 5), (3, 4, 6)])
+@pytest.mark.parametrize("world,every,steps", [(2, 1, 3), (2, 2, 5), (3, 4, 6), (8, 2, 5)])
 def test_bench_pipe_grouped_gather(world, every, steps):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
