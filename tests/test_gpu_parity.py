@@ -351,6 +351,89 @@ def test_var_packets_at_view_start(W, VAR, lead):
     assert np.array_equal(to_u32(out, n), O.batch_var(host[lead:], offs, lens))
 
 
+def _fuzz_layout(rng):
+    """One random mixed-length batch: a length distribution, a layout (packed, packed with
+    gaps, unordered and overlapping, or runs of equal offsets) and a view lead."""
+    n = int(rng.integers(1, 6000))
+    kind = rng.choice(["uniform", "zipf", "tiny", "bimodal", "long", "rows"])
+    if kind == "uniform":
+        lens = rng.integers(0, 1457, n)
+    elif kind == "zipf":
+        lens = O.zipf_lengths(n, s=float(rng.choice([1.0, 1.1, 1.3])), seed=int(rng.integers(1 << 30)))
+    elif kind == "tiny":
+        lens = rng.integers(0, 17, n)
+    elif kind == "bimodal":
+        lens = np.where(rng.random(n) < 0.6, rng.integers(0, 33, n), rng.integers(1000, 1457, n))
+    elif kind == "long":
+        lens = rng.integers(1400, 4097, n)
+    else:  # lengths at and around 64-B piece and 256-B row boundaries
+        lens = rng.choice([1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1455, 1456], n)
+    lens = np.asarray(lens, dtype=np.uint32)
+    layout = rng.choice(["packed", "gaps", "unordered", "runs"])
+    if layout in ("packed", "gaps"):
+        gap = rng.integers(0, 40, n) if layout == "gaps" else np.zeros(n, np.int64)
+        ends = np.cumsum(lens.astype(np.uint64) + gap.astype(np.uint64))
+        offs = (ends - lens).astype(np.uint64)
+        total = int(ends[-1]) if n else 1
+    else:
+        total = int(lens.sum()) + 5000
+        offs = rng.integers(0, max(1, total - 4097), n).astype(np.uint64)
+        if layout == "runs":
+            offs = np.repeat(offs[::7], 7)[:n]
+        total = max(total, int((offs + lens).max()))
+    return lens, offs, max(total, 1), int(rng.integers(0, 64)), str(kind), str(layout)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_var_fuzz_random_layouts(W, VAR, seed):
+    """Seeded random batches through every route (piece kernel with LDS-DMA staging, its
+    span-miss reloads, the packed and stream routes) vs the oracle, element-wise."""
+    rng = np.random.default_rng(1000 + seed)
+    for _ in range(4):
+        lens, offs, total, lead, kind, layout = _fuzz_layout(rng)
+        host = O.synth_fill_np(lead + total, start_byte=int(rng.integers(1 << 20)))
+        d = dev_u8(host)
+        n = lens.size
+        out = u32_out(n)
+        VAR(d[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+            torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+        want = O.batch_var(host[lead:], offs, lens)
+        got = to_u32(out, n)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (kind, layout, n, lead, bad[:5])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_verify_fuzz_random_rings(W, seed):
+    """Seeded random datagram rings (stride a multiple of 16 or not, any recv_len including
+    runts, oversize and full slots, bit flips in payload and header) vs the oracle."""
+    rng = np.random.default_rng(2000 + seed)
+    for _ in range(3):
+        stride = int(rng.choice([1472, 1488, 1504, 1500, 1473, 64, 1024, 2048]))
+        n = int(rng.integers(1, 5000))
+        buf = O.synth_fill_np(n * stride, start_byte=int(rng.integers(1 << 20))).copy()
+        rl = np.empty(n, np.uint32)
+        for i in range(n):
+            r = rng.random()
+            L = stride if r < 0.5 else (int(rng.integers(0, 16)) if r < 0.6 else
+                                       (stride + int(rng.integers(1, 40)) if r < 0.65 else int(rng.integers(16, stride + 1))))
+            rl[i] = L
+            if 16 <= L <= stride and rng.random() < 0.8:  # a valid checksum for its bytes
+                crc = O.crc32(buf[i * stride + 16:i * stride + L])
+                buf[i * stride + 12:i * stride + 16] = np.frombuffer(int(crc).to_bytes(4, "big"), np.uint8)
+            if L > 16 and rng.random() < 0.1:
+                buf[i * stride + 16 + int(rng.integers(0, min(L, stride) - 16))] ^= np.uint8(0x40)
+        want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+        d = dev_u8(buf)
+        r = torch.from_numpy(rl.view(np.int32)).cuda()
+        ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        crc = u32_out(n)
+        W.verify_batch(d, stride, r, n, ok, crc)
+        torch.cuda.synchronize()
+        assert np.array_equal(ok.cpu().numpy(), want_ok), (stride, n)
+        assert np.array_equal(to_u32(crc, n), want_crc), (stride, n)
+
+
 def test_var_bad_length_large_batch_sets_status(W, VAR):
     W.device_status(0, clear=True)
     n = 70_000
