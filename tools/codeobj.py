@@ -93,7 +93,7 @@ def kernel_code_sha256(lib_path: str, pattern: str) -> dict:
 
 
 # the headline kernel: k_fixed_braid<6 rows, DIAG 0, CrcBEpi> (1456-B payloads)
-HEADLINE_KERNEL = r"k_fixed_braidILi6ELi0ENS\w*CrcBEpi"
+HEADLINE_KERNEL = r"k_fixed_braidILi6ELi0ENS0_7CrcBEpiE"
 
 if __name__ == "__main__":
     import json

@@ -37,6 +37,9 @@ for s in $STEPS; do
     testslib) for t in ${TEST_LIBS}; do
              WTP_LIB="$ROOT/a3-reliable-transport_amd/lib/ab/$t.so" run "gpu_tests_$t" 600 python -u -m pytest tests -m gpu -x -v -rf --timeout=300 --timeout-method thread -k "${TEST_K:-not loopback and not bench_}"
            done ;;
+    abcrcns) for nn in ${AB_NS:-16384 65536 262144 1048576}; do
+               run "abcrc_n$nn" 300 python tools/ab_lib.py --what crc --n $nn ${AB_LIBS}
+             done ;;
     abcrcalt) run abcrcalt 300 python tools/ab_lib.py --what crcalt --n ${AB_N:-1048576} ${AB_LIBS} ;;
     abcrc2m) run abcrc2m 300 python tools/ab_lib.py --what crc --n 2097152 ${AB_LIBS} ;;
     c5sq)  for lib in ${SQ_LIBS:-product}; do
