@@ -786,17 +786,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 __device__ __forceinline__ uint32_t pieces_of_len(uint32_t len) {
     return (len == 0 || len > kMaxVarLen) ? 1u : (len + kPieceS - 1) / kPieceS;
 }
-// The wave split's work units of a packet: its pieces, or with tiny rounds (Prov::kTiny)
-// 4 per piece and 1 per tiny packet (a 4-word chain in a round shared by 64 of them).
-// Never 0, so every workgroup's total is at least its packet count.
-template <class Prov>
-__device__ __forceinline__ uint32_t split_units(uint32_t len) {
-    if constexpr (Prov::kTiny) return len <= 15u ? 1u : 4u * pieces_of_len(len);
-    return pieces_of_len(len);
-}
 template <class Prov>
 __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
-    return split_units<Prov>(prov.len_of(prov.load_len(p)));
+    return pieces_of_len(prov.len_of(prov.load_len(p)));
 }
 
 // Wave ranges of a workgroup's packets [g0, g1) with equal piece counts (rounds), not
@@ -848,7 +840,7 @@ struct WaveSplit {
         uint32_t k[kReg], sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kReg; ++j) {
-            k[j] = j < m ? split_units<Prov>(prov.len_of(raw[j])) : 0u;
+            k[j] = j < m ? pieces_of_len(prov.len_of(raw[j])) : 0u;
             sum += k[j];
         }
         for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p);  // > kReg per thread
@@ -925,20 +917,6 @@ __device__ __forceinline__ void load_span(__amdgpu_buffer_rsrc_t rs, int32_t b16
 #ifndef WTP_PC_DMA
 #define WTP_PC_DMA 1  // 0: register staging (load_span + ds_write_b128), the round-3 form (A/B builds)
 #endif
-#ifndef WTP_PC_TINY
-#define WTP_PC_TINY 0  // offset/length arrays: packets <= 15 B leave the piece stream for tiny rounds
-#endif
-constexpr uint32_t kTinyMax = 15;  // tiny packets: 0..15 B (the length shares a word with a 28-bit index)
-// Inclusive prefix max over the wave with DPP (as wave_incl_add).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false)));
-    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false)));
-    return v;
-}
 constexpr uint32_t kPcSlotPos = kPcSlot / 16;                 // 290 positions of 16 B
 constexpr uint32_t kPcDmaRegs = (kPcSlotPos + 63) / 64;       // 5 instructions
 static_assert(kPcSlotPos - 64 * (kPcDmaRegs - 1) <= 64, "slot positions");
@@ -1035,76 +1013,6 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
 #endif
     uint32_t nrounds = 0, done = 0;
     hi = uniform64(hi);  // wave-uniform in SGPRs: the round's packet arithmetic stays scalar
-
-    // Tiny rounds (Prov::kTiny: packets of 0..15 B).  Such a packet takes no lane of the
-    // piece stream (0 pieces).  The round that consumes it queues (end offset, index | len
-    // << 28) in two banks of 64 lane entries; when 64 are queued, their 16-B windows (the
-    // bytes ending at each packet end, one unaligned buffer load per lane) are loaded
-    // there and hashed one round later: a 4-word slice-by-4 chain with the bytes before
-    // the packet masked, + shift(~0, len) from the head-init table.  64 tiny packets then
-    // cost one 4-word chain instead of 64 lanes of 16-word chains.
-    uint32_t tq_e0 = 0, tq_l0 = 0, tq_e1 = 0, tq_l1 = 0;  // queue banks: end offset, idx | len << 28
-    uint32_t tqn = 0;                                      // queued entries (wave-uniform, < 64 between rounds)
-    uint32_t tp_l = 0, tp_n = 0;                           // pending tiny round: entry per lane, count
-    bool tp_fresh = false;                                 // fired in this round (its loads just issued)
-    u32x4 tp_w = {0u, 0u, 0u, 0u};
-    auto tiny_compute = [&]() {
-        if (tp_n == 0) return;  // wave-uniform
-        const uint32_t tlen = tp_l >> 28;
-        const int32_t tvf8 = 8 * int32_t(16u - tlen);
-        const uint32_t w[4] = {tp_w.x, tp_w.y, tp_w.z, tp_w.w};
-        uint32_t c = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int32_t t = tvf8 < 32 * i ? 32 * i : (tvf8 > 32 * i + 32 ? 32 * i + 32 : tvf8);
-            const uint64_t k64 = uint64_t(0xFFFFFFFFu) << (uint32_t(t) & 63u);
-            const uint32_t keep = (i & 1) ? uint32_t(k64 >> 32) : uint32_t(k64);
-            c = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(c, w[i], keep, 0x78));
-        }
-        const uint32_t crc = c ^ lds_rd(lds, kPcHinit + 4u * tlen) ^ 0xFFFFFFFFu;
-        epi.put(uint64_t(tp_l & 0x0FFFFFFFu), crc, true, 0u, lane < tp_n);
-        tp_n = 0;
-    };
-    auto tiny_fire = [&](uint32_t cnt) {  // bank 0's first cnt entries -> the pending round
-        if (tp_n) tiny_compute();           // the previous round's (its loads have landed)
-        tp_w = buf_ld16(rs, lane < cnt ? tq_e0 - 16u : 0x80000000u);
-        tp_l = tq_l0;
-        tp_n = cnt;
-        tp_fresh = true;
-    };
-    // queue the lanes with t set (packets of the view, in lane order): they go to entries
-    // tqn, tqn + 1, ... through the (already used) flag bytes of the wave
-    auto tiny_enqueue = [&](bool t, uint32_t te, uint32_t tl_) {
-        const uint64_t m = __ballot(t);
-        const uint32_t cnt = uint32_t(__popcll(m));  // wave-uniform
-        if (cnt == 0) return;
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-        lu8 *const tf = (lu8 *)lds + kPcFlags + wave * 64u;
-        __builtin_amdgcn_wave_barrier();
-        if (t) tf[rank] = uint8_t(lane);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t s0 = tf[(lane - tqn) & 63u];
-        const uint32_t ne0 = __shfl(te, int(s0)), nl0 = __shfl(tl_, int(s0));
-        const bool take0 = lane >= tqn && lane < tqn + cnt;
-        tq_e0 = take0 ? ne0 : tq_e0;
-        tq_l0 = take0 ? nl0 : tq_l0;
-        if (tqn + cnt > 64u) {  // wave-uniform: the rest goes to bank 1
-            const uint32_t s1 = tf[(lane + 64u - tqn) & 63u];
-            const uint32_t ne1 = __shfl(te, int(s1)), nl1 = __shfl(tl_, int(s1));
-            const bool take1 = lane + 64u < tqn + cnt;
-            tq_e1 = take1 ? ne1 : tq_e1;
-            tq_l1 = take1 ? nl1 : tq_l1;
-        }
-        __builtin_amdgcn_wave_barrier();
-        tqn += cnt;
-        if (tqn >= 64u) {
-            tiny_fire(64u);
-            tq_e0 = tq_e1;
-            tq_l0 = tq_l1;
-            tqn -= 64u;
-        }
-        done += cnt;
-    };
     for (uint64_t p0 = uniform64(lo); p0 < hi;) {
         uint64_t off;
         uint32_t len, aux = 0, oslot = 0;
@@ -1117,47 +1025,24 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             len = 0;
             valid = false;
         }
-        const uint32_t tend = uint32_t(off) + len;  // tiny rounds: the packet end (view < 2 GiB)
-        const bool tiny = Prov::kTiny && have && valid && len <= kTinyMax && tend >= 16u;
-        const uint32_t k = have ? (tiny ? 0u : (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS)) : 64u;
+        const uint32_t k = have ? (len == 0 ? 1u : (len + kPieceS - 1) / kPieceS) : 64u;
         const uint32_t kr = k - (lane == 0 ? skip : 0u);  // pieces still to do
         const uint32_t incl = wave_incl_add(kr);
         const uint32_t excl = incl - kr;
         const uint32_t navail = __popcll(__ballot(have));  // packets of the wave left in view
         const uint32_t covered = uint32_t(__builtin_amdgcn_readlane(int(incl), int(navail - 1)));  // pieces in view
-        const uint32_t tli = uint32_t(p0 + lane) | (len << 28);  // tiny queue entry: index | len << 28
-        if constexpr (Prov::kTiny) {
-            if (covered == 0) {  // wave-uniform: only tiny packets in view
-                tiny_enqueue(tiny, tend, tli);
-                if (tp_n && !tp_fresh) tiny_compute();
-                tp_fresh = false;
-                p0 = uniform64(p0 + navail);
-                meta(p0);
-                continue;
-            }
-        }
 
         // --- lane -> (packet, piece): flag the first lane of every packet in LDS, then
-        // pk = (# flagged lanes <= this lane) - 1 from a ballot (with tiny packets, which
-        // have no piece: the flag holds the packet's lane, pk = the prefix max) -------------
+        // pk = (# flagged lanes <= this lane) - 1 from a ballot ----------------------------
         lu8 *const flags = (lu8 *)lds + kPcFlags + wave * 64u;
-        uint32_t pk;
-        if constexpr (Prov::kTiny) {
-            flags[lane] = 0;
-            if (have && kr > 0u && excl < 64u) flags[excl] = uint8_t(lane);
-            __builtin_amdgcn_wave_barrier();
-            pk = wave_incl_max(flags[lane]);
-            __builtin_amdgcn_wave_barrier();
-        } else {
-            flags[lane] = 0;
-            if (have && excl < 64u) flags[excl] = 1;
-            __builtin_amdgcn_wave_barrier();
-            const bool start = flags[lane] != 0;
-            __builtin_amdgcn_wave_barrier();
-            const uint64_t starts = __ballot(start);
-            pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
-                 (start ? 1u : 0u) - 1u;
-        }
+        flags[lane] = 0;
+        if (have && excl < 64u) flags[excl] = 1;
+        __builtin_amdgcn_wave_barrier();
+        const bool start = flags[lane] != 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t starts = __ballot(start);
+        uint32_t pk = __builtin_amdgcn_mbcnt_hi(uint32_t(starts >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(starts), 0u)) +
+                      (start ? 1u : 0u) - 1u;
         const bool mapped = lane < covered;
         pk = mapped ? pk : 0;
         const uint32_t pex = __shfl(excl, pk);
@@ -1235,7 +1120,6 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
 #else
         load_span(rs, spec, lane, x);
 #endif
-        if constexpr (Prov::kTiny) tiny_enqueue(tiny && lane < uint32_t(p0n - p0), tend, tli);
 
         // rotate left by a>>2 dwords with bit-selects (v_bfi_b32), then funnel by a&3
         const uint32_t a = uint32_t(ws) & 15u;
@@ -1294,10 +1178,6 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             if (need) W = op_apply_fold(lds, kPcOps + (o + kPcNOps - 5) * kOpBytes, u, W);  // exec-masked: idle lanes issue no lookups
         }
         epi.put(pout, W ^ 0xFFFFFFFFu, pvalid, paux, active && gp == pkk - 1);
-        if constexpr (Prov::kTiny) {
-            if (tp_n && !tp_fresh) tiny_compute();
-            tp_fresh = false;
-        }
         carry = partial ? __builtin_amdgcn_readlane(W, tl) : 0u;
         skip = partial ? last_gp + 1 : 0u;
         p0 = uniform64(p0n);  // keeps the loop-carried packet index in SGPRs
@@ -1308,7 +1188,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             // fixed rotation the youngest waves still ended ~8 us after the oldest
             // (tools/pprobe.py).  Priority = how many of the SIMD's four waves have less
             // work left than this one (stale reads only blur the ranking).
-            done += Prov::kTiny ? 4u * total : total;  // the split's units
+            done += total;
             const uint32_t left = wpieces > done ? wpieces - done : 0u;
             const uint32_t simd = wave & 3u;
             typedef __attribute__((address_space(3))) uint32_t lu32w;
@@ -1318,13 +1198,6 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             rotate_prio(uint32_t(__popcll(__builtin_amdgcn_ballot_w64(lane < kPcWaves / 4u && other < left))));
         } else {
             rotate_prio(nrounds + (wave >> 2));
-        }
-    }
-    if constexpr (Prov::kTiny) {  // the last tiny rounds: the pending one, then what is queued
-        if (tp_n) tiny_compute();
-        if (tqn) {
-            tiny_fire(tqn);
-            tiny_compute();
         }
     }
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
@@ -1446,7 +1319,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 // pprobe) define WTP_AB_BUILD to build variants.  A misconfigured product build is a
 // compile error, not a library that runs wrong.
 #ifndef WTP_AB_BUILD
-static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1 && WTP_PC_TINY == 0,
+static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
@@ -1461,7 +1334,6 @@ struct LdsIdxDgramProv {
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
     static constexpr bool kGroupLoad = false;
-    static constexpr bool kTiny = false;  // see pieces_loop's tiny-packet rounds
     uint64_t stride;
     const uint32_t *__restrict__ rl;
     const lu32 *list;
@@ -2170,7 +2042,6 @@ struct FixedProvL {
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = false;
-    static constexpr bool kTiny = false;  // see pieces_loop's tiny-packet rounds
     uint64_t stride, lead;
     uint32_t len;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const { r.a = p; }
@@ -2185,7 +2056,6 @@ struct ArrayProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = true;  // load_group: 32-bit buffer offsets, no clamp
-    static constexpr bool kTiny = WTP_PC_TINY;  // packets <= 15 B in tiny rounds (pieces_loop)
     const uint64_t *__restrict__ offs;
     const uint32_t *__restrict__ lens;
     uint64_t lead;
@@ -2220,7 +2090,6 @@ struct DgramProvL {
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = false;
-    static constexpr bool kTiny = false;  // see pieces_loop's tiny-packet rounds
     uint64_t stride, lead;
     const uint32_t *__restrict__ rl;
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t rs) const {
