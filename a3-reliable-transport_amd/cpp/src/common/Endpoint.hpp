@@ -69,7 +69,7 @@ class Log {
 class Checksums {
    public:
     // Receiver batches of at most this many payload bytes are verified on the CPU in GPU
-    // mode (crc32_fast): below it one GPU call (launch + sync, ~25 us from the host)
+    // mode (crc32_fast): below it one GPU call (launch + sync + PCIe, ~21 us from C++)
     // costs more than hashing the bytes here.  Measured crossover on the MI355X box:
     // DESIGN.md 5 (tools/verify_crossover.cpp); WTP_VERIFY_CPU_MAX_BYTES overrides it
     // (0 = always the GPU).

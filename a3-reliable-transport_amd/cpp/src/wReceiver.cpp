@@ -23,9 +23,10 @@
 // ring of --batch slots (default: the window size), the whole batch is verified with one
 // call (one GPU launch with --crc gpu; batches of at most Checksums::kCpuVerifyMaxBytes
 // of payload are hashed on the CPU with crc32_fast instead, where a GPU call's launch and
-// sync cost more), then processed in arrival order exactly as one-at-a-time reception would.  --bench measures that path alone: it receives DATA
-// datagrams (e.g. from wBlast) for the given seconds, verifying each batch on a worker
-// thread while the next one arrives, and prints one JSON line with the rate.
+// sync cost more), then processed in arrival order exactly as one-at-a-time reception
+// would.  --bench measures that path alone: it receives DATA datagrams (e.g. from wBlast)
+// for the given seconds, verifying each batch on a worker thread while the next one
+// arrives, and prints one JSON line with the rate.
 #include <time.h>
 
 #include <condition_variable>
