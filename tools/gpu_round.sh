@@ -128,6 +128,10 @@ for s in $STEPS; do
     abcrc) run abcrc 300 python tools/ab_lib.py --what crc --n ${AB_N:-1048576} ${AB_LIBS} ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    kbalt) for al in 0 1; do  # braided kernel, its ablations and the probes: one buffer vs alternating buffers
+             KB_ALT=$al KB_ONLY="${KB_VARS:-braid512_prod,braid512_skel,braid512_nolut,braid512_nofold,braid512_noprio,read_probe_g256x512,strided_nt_d2_g512}" \
+               KB_SUSTAIN=all KB_REPS=${KB_REPS:-3} KB_NS=${KB_NS:-100} run "kbalt$al" 200 ./tools/bin/kbench ${KB_N:-1048576} 10
+           done ;;
   esac
 done
 echo "done" | tee -a "$OUT/steps.log"

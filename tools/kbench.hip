@@ -211,10 +211,15 @@ int main(int argc, char **argv) {
     CK(hipSetDevice(0));
     if (wtp_init(0)) { fprintf(stderr, "init: %s\n", wtp_last_error()); return 1; }
     DevState &s = g_dev[0];
-    uint8_t *buf; uint32_t *out;
-    CK(hipMalloc(&buf, bytes + 64));
+    // KB_ALT=1: two n-packet buffers, every launch reads the other one (no launch re-reads
+    // what the previous launch read: the streaming case)
+    const bool alt = getenv("KB_ALT") && atoi(getenv("KB_ALT"));
+    uint8_t *base0, *buf; uint32_t *out;
+    CK(hipMalloc(&base0, (alt ? 2 : 1) * bytes + 64));
     CK(hipMalloc(&out, n * 4 + 64));
-    if (wtp_synth_fill(buf, 0, bytes, 0x5EED, nullptr)) return 1;
+    if (wtp_synth_fill(base0, 0, (alt ? 2 : 1) * bytes, 0x5EED, nullptr)) return 1;
+    buf = base0;
+    auto flip = [&] { if (alt) buf = buf == base0 ? base0 + bytes : base0; };
     CK(hipDeviceSynchronize());
     const uint32_t cinit = init_const(1456);
     const uint64_t rounds = (n + 3) / 4;
@@ -232,6 +237,12 @@ int main(int argc, char **argv) {
     const unsigned grid512 = unsigned(std::min<uint64_t>((rounds + 7) / 8, s.cus));
 #define BD5(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
     BD5("braid512_noprio", 4); BD5("braid512_prod", 0); BD5("braid512_nolut", 1); BD5("braid512_nofold", 2); BD5("braid512_skel", 3);
+    // grid pacing (DIAG bit3): its counters are zeroed before every launch, so
+    // the control variant pays the same memset
+    void *drift = nullptr;
+    CK(hipGetSymbolAddress(&drift, HIP_SYMBOL(g_drift)));
+#define BDM(NAME, DIAG) vs.push_back({NAME, [&] { (void)hipMemsetAsync(drift, 0, 4096, 0); hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
+    BDM("braid512_ms", 0); BDM("varbraid512_pace", 8); BDM("braid512_skel_ms", 3); BDM("braid512_skel_pace", 11);
     vs.push_back({"read_probe_g256x512", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(512), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_nt_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
@@ -261,10 +272,11 @@ int main(int argc, char **argv) {
     }
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-    for (auto &v : vs) { v.f(); v.f(); }
+    for (auto &v : vs) { flip(); v.f(); flip(); v.f(); }
     CK(hipDeviceSynchronize());
     for (int r = 0; r < reps; ++r)
         for (auto &v : vs) {
+            flip();
             CK(hipEventRecord(a, 0));
             v.f();
             CK(hipEventRecord(b, 0));
@@ -288,7 +300,7 @@ int main(int argc, char **argv) {
             CK(hipDeviceSynchronize());
             usleep(200000);  // let clocks settle between variants
             CK(hipEventRecord(ev[0], 0));
-            for (int r = 0; r < NS; ++r) { v.f(); CK(hipEventRecord(ev[r + 1], 0)); }
+            for (int r = 0; r < NS; ++r) { flip(); v.f(); CK(hipEventRecord(ev[r + 1], 0)); }
             CK(hipDeviceSynchronize());
             std::vector<float> t;
             for (int r = 0; r < NS; ++r) { float ms; CK(hipEventElapsedTime(&ms, ev[r], ev[r + 1])); t.push_back(ms); }
@@ -315,6 +327,7 @@ int main(int argc, char **argv) {
         std::vector<hipEvent_t> ev(2 * reps);
         for (size_t k = 0; k < ev.size(); ++k) CK(hipEventCreate(&ev[k]));
         for (int r = 0; r < reps; ++r) {
+            flip();
             CK(hipEventRecord(ev[2 * r], 0));
             vs[bp].f();
             CK(hipEventRecord(ev[2 * r + 1], 0));
@@ -327,6 +340,7 @@ int main(int argc, char **argv) {
                bytes / (t[t.size() / 2] * 1e-3) / 1e9, t[0], t.back());
     }
     {  // correctness of the var* variants against braid_prod (same outputs, bit-exact)
+        buf = base0;
         std::vector<uint32_t> ref(n), got(n);
         size_t bp = 0;
         for (size_t k = 0; k < vs.size(); ++k) if (!strcmp(vs[k].name, "braid_prod")) bp = k;
@@ -341,7 +355,8 @@ int main(int argc, char **argv) {
             printf("CHECK %-20s %s (%llu mismatches)\n", v.name, bad ? "MISMATCH" : "ok", (unsigned long long)bad);
         }
     }
-    printf("# n=%llu packets x 1456 B = %.3f GB per launch, grid(braid)=%u, reps=%d\n", (unsigned long long)n, bytes / 1e9, grid, reps);
+    printf("# n=%llu packets x 1456 B = %.3f GB per launch, grid(braid)=%u, reps=%d, %s\n", (unsigned long long)n, bytes / 1e9, grid, reps,
+           alt ? "alternating buffers (KB_ALT)" : "one buffer");
     for (auto &v : vs) {
         std::sort(v.t.begin(), v.t.end());
         const float med = v.t[v.t.size() / 2], mn = v.t[0];
