@@ -481,7 +481,7 @@ __device__ uint32_t g_drift[1024];  // per-block finish counts (zeroed by the ca
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
-                                                      const uint32_t *__restrict__ gtab, uint32_t fronts) {
+                                                      const uint32_t *__restrict__ gtab) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kBraidLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
     constexpr uint32_t kGroup = 8;  // rounds per flush (2 KiB slot per wave)
@@ -495,26 +495,13 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     const StagKeys K(lane);
 
     constexpr uint32_t kFrame = 256u * ROWS;
+    const uint64_t rounds = (n + 3) >> 2;
     // Round order: grid-interleaved, wave (b, w) takes rounds b*nwave + w + i*rstep, so the
     // whole grid moves through the batch as one front.  (A contiguous block of rounds per
     // workgroup, and one per XCD class b % 8, were built in round 4 and measured slower at
     // every size, DESIGN 7.10, as was a translation-prefetch wave; code in git history,
-    // commits f56e6d4 and 8c994a0.)  With fronts = F > 1 (the launcher's rule for batches
-    // larger than one front's span, gridDim.x a multiple of 8F) the rounds are cut into F
-    // contiguous parts and the grid into F sub-grids, each with the same number of
-    // workgroups on every XCD; each sub-grid walks its part as one front, so a CU touches
-    // the address translations of 1/F of the batch.
-    uint64_t rlo = 0, rounds = (n + 3) >> 2;  // this front's rounds [rlo, rounds)
-    uint32_t bi = blockIdx.x, gsub = gridDim.x;
-    if (fronts > 1) {
-        const uint32_t f = (blockIdx.x >> 3) % fronts;
-        bi = ((blockIdx.x >> 3) / fronts) * 8u + (blockIdx.x & 7u);
-        gsub = gridDim.x / fronts;
-        const uint64_t all = rounds;
-        rlo = all * f / fronts;
-        rounds = all * (f + 1) / fronts;
-    }
-    const uint64_t rstep = uint64_t(gsub) * nwave;
+    // commits f56e6d4 and 8c994a0.)
+    const uint64_t rstep = uint64_t(gridDim.x) * nwave;
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -632,7 +619,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if (++k == kGroup) flush(rr + rstep, true);
     };
 
-    uint64_t r = rlo + uint64_t(bi) * nwave + wave;
+    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
@@ -2005,16 +1992,10 @@ static_assert(dev::VerifyBEpi::kThreads == 64 * dev::kVfWaves, "verify fix-up LD
 
 template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
-                       uint64_t n, BEpi epi, const uint32_t *tabs, uint32_t fronts) {
+                       uint64_t n, BEpi epi, const uint32_t *tabs) {
     hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, BEpi::kDiag, BEpi>), grid, dim3(threads), 0, st, b,
-                       uint32_t(stride), len, n, epi, tabs, fronts);
+                       uint32_t(stride), len, n, epi, tabs);
 }
-
-// Bytes one front of the braided CRC walks at most (k_fixed_braid's round order): a batch
-// larger than this runs as ceil(bytes / span) fronts.  1 M x 1456 B (1.53 GB) is one front.
-#ifndef WTP_BR_FRONT_BYTES
-#define WTP_BR_FRONT_BYTES 1000000000000ull  // one front until the A/B says otherwise
-#endif
 
 // Braided kernel over n packets base[p*stride, +len): base, stride, len multiples of 16,
 // 16 <= len <= 1536, stride <= 16 KiB.  The epilogue's cinit is filled in here.
@@ -2033,27 +2014,15 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
     // batches keep every CU (C2: 8 rounds per wave, a ninth would be its tail).
     if (!BEpi::kCopy && s.reserve.load(std::memory_order_relaxed) == 0 && rounds >= 64 * cap * (threads / 64))
         cap -= cap / 32;
-    unsigned grid = unsigned(want < cap ? want : cap);
-    // several fronts (CRC only: the verify fix-up and the builder assume one), each with
-    // the same number of workgroups per XCD
-    uint32_t fronts = 1;
-    if (!BEpi::kCopy && !BEpi::kFixup && rounds >= 64 * uint64_t(grid) * (threads / 64)) {
-        const uint64_t bytes = n * stride;
-        uint64_t f = (bytes + WTP_BR_FRONT_BYTES - 1) / WTP_BR_FRONT_BYTES;
-        while (f > 1 && grid < 8 * f) --f;
-        if (f > 1) {
-            fronts = uint32_t(f);
-            grid = unsigned(grid / (8 * f) * (8 * f));
-        }
-    }
+    const unsigned grid = unsigned(want < cap ? want : cap);
     epi.cinit = init_const(len);
     switch (rows) {
-        case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
-        case 2: launch_braid_rows<2>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
-        case 3: launch_braid_rows<3>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
-        case 4: launch_braid_rows<4>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
-        case 5: launch_braid_rows<5>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
-        case 6: launch_braid_rows<6>(grid, threads, st, base, stride, len, n, epi, s.tabs, fronts); break;
+        case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 2: launch_braid_rows<2>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 3: launch_braid_rows<3>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 4: launch_braid_rows<4>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 5: launch_braid_rows<5>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
+        case 6: launch_braid_rows<6>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
         default: return fail(WTP_EINVAL, "braid rows %d", rows);
     }
     return launch_check("k_fixed_braid");

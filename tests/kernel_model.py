@@ -363,46 +363,3 @@ def stream_wave(T: StreamTables, buf: bytes, offs, lens, view_addr: int = 0):
         R += ST_ROUND
         rounds += 1
     return out, rounds
-
-
-# ---- k_fixed_braid round order (launch_fixed_braid's grid/front rule + the kernel's map) ----
-FRONT_BYTES = 1_000_000_000_000  # WTP_BR_FRONT_BYTES
-
-
-def braid_launch(n: int, stride: int, cus: int = 256, threads: int = 512, reserve: int = 0, crc: bool = True,
-                 front_bytes: int = FRONT_BYTES):
-    """(grid, fronts) as launch_fixed_braid chooses them for n packets."""
-    waves = threads // 64
-    rounds = (n + 3) // 4
-    want = (rounds + waves - 1) // waves
-    cap = max(1, cus - reserve)
-    if crc and reserve == 0 and rounds >= 64 * cap * waves:
-        cap -= cap // 32
-    grid = min(want, cap)
-    fronts = 1
-    if crc and rounds >= 64 * grid * waves:
-        f = (n * stride + front_bytes - 1) // front_bytes
-        while f > 1 and grid < 8 * f:
-            f -= 1
-        if f > 1:
-            fronts, grid = f, grid // (8 * f) * (8 * f)
-    return grid, fronts
-
-
-def braid_wave_rounds(n: int, grid: int, fronts: int, threads: int = 512):
-    """Rounds (groups of 4 packets) each wave (block, wave) hashes, as k_fixed_braid walks
-    them: {(block, wave): [round, ...]}."""
-    nwave = threads // 64
-    out = {}
-    for b in range(grid):
-        rlo, rounds, bi, gsub = 0, (n + 3) // 4, b, grid
-        if fronts > 1:
-            f = (b >> 3) % fronts
-            bi = ((b >> 3) // fronts) * 8 + (b & 7)
-            gsub = grid // fronts
-            allr = rounds
-            rlo, rounds = allr * f // fronts, allr * (f + 1) // fronts
-        rstep = gsub * nwave
-        for w in range(nwave):
-            out[(b, w)] = list(range(rlo + bi * nwave + w, rounds, rstep))
-    return out

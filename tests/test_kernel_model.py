@@ -85,31 +85,3 @@ def test_stream_model(case):
         buf = O.synth_fill_np(int(offs[-1] + lens[-1]) + 9, start_byte=first).tobytes()
         out, _ = K.stream_wave(T, buf, offs, lens, view_addr=view_addr)
         assert out == [O.crc32(buf[o:o + L]) for o, L in zip(offs, lens)], (case, first)
-
-
-@pytest.mark.parametrize("front_bytes", [None, 1_600_000_000, 800_000_000])
-@pytest.mark.parametrize("n,reserve", [(1 << 20, 0), (2 << 20, 0), (2 << 20, 8), (3_200_000, 0), (65536, 0), (5, 0)])
-def test_braid_round_order_covers_every_round_once(n, reserve, front_bytes):
-    """The braided kernel's round order (one front, or F fronts for batches larger than
-    WTP_BR_FRONT_BYTES: the shipped value and two smaller ones) hands every round of the
-    batch to exactly one wave, and every front has the same number of workgroups on each
-    XCD (block % 8)."""
-    from kernel_model import FRONT_BYTES, braid_launch, braid_wave_rounds
-    fb = front_bytes or FRONT_BYTES
-    grid, fronts = braid_launch(n, 1456, reserve=reserve, front_bytes=fb)
-    if n * 1456 <= fb or n < 1 << 20:
-        assert fronts == 1
-    else:
-        assert fronts == -(-n * 1456 // fb) and grid % (8 * fronts) == 0
-    owner = braid_wave_rounds(n, grid, fronts)
-    seen = np.zeros((n + 3) // 4, dtype=np.int32)
-    for rs in owner.values():
-        seen[rs] += 1
-    assert (seen == 1).all()
-    if fronts == 1:
-        return
-    per = {}
-    for b in range(grid):
-        f = (b >> 3) % fronts
-        per.setdefault(f, np.zeros(8, int))[b & 7] += 1
-    assert all((v == v[0]).all() for v in per.values()) and len({int(v[0]) for v in per.values()}) == 1

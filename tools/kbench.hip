@@ -230,18 +230,18 @@ int main(int argc, char **argv) {
     vs.push_back({"read_probe_g256x1024", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(1024), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g2048x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(2048), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"read_probe_g8192x256", [&] { hipLaunchKernelGGL(k_read_probe, dim3(8192), dim3(256), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
-    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs, 1u); }, {}});
-#define BD(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs, 1u); }, {}})
+    vs.push_back({"braid_prod", [&] { hipLaunchKernelGGL(k_fixed_braid<6>, dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}});
+#define BD(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid), dim3(1024), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
     BD("braid_nolut", 1); BD("braid_nofold", 2); BD("braid_skel", 3);
     // the product's workgroup size (512 threads, 8 waves per CU) and its ablations
     const unsigned grid512 = unsigned(std::min<uint64_t>((rounds + 7) / 8, s.cus));
-#define BD5(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs, 1u); }, {}})
+#define BD5(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
     BD5("braid512_noprio", 4); BD5("braid512_prod", 0); BD5("braid512_nolut", 1); BD5("braid512_nofold", 2); BD5("braid512_skel", 3);
     // grid pacing (DIAG bit3): its counters are zeroed before every launch, so
     // the control variant pays the same memset
     void *drift = nullptr;
     CK(hipGetSymbolAddress(&drift, HIP_SYMBOL(g_drift)));
-#define BDM(NAME, DIAG) vs.push_back({NAME, [&] { (void)hipMemsetAsync(drift, 0, 4096, 0); hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs, 1u); }, {}})
+#define BDM(NAME, DIAG) vs.push_back({NAME, [&] { (void)hipMemsetAsync(drift, 0, 4096, 0); hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
     BDM("braid512_ms", 0); BDM("varbraid512_pace", 8); BDM("braid512_skel_ms", 3); BDM("braid512_skel_pace", 11);
     vs.push_back({"read_probe_g256x512", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(512), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
