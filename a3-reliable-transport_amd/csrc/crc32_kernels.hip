@@ -468,16 +468,10 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // stored once per 8 rounds (on gfx950 stores share vmcnt with loads).
 //
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
-// XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation,
-// bit3 paces the grid (no wave starts iteration block k + kDriftLag before every wave has
-// finished block k; blocks of 8 iterations, counters in g_drift, bounded waits).
+// XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation;
+// access-pattern ablations: bit4 drops the result stores, bit5 loads row 0
+// nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len).
 // Production instantiations use DIAG = 0.
-#ifdef WTP_AB_BUILD
-__device__ uint32_t g_drift[1024];  // per-block finish counts (zeroed by the caller per launch)
-#ifndef WTP_DRIFT_LAG
-#define WTP_DRIFT_LAG 2
-#endif
-#endif
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
@@ -517,7 +511,8 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         const uint64_t last = live ? n - 1 - p0 : 0;
         const uint32_t nrec = !live ? 0u : (last >= 3 ? 3u * stride + len : uint32_t(last) * stride + len);
         const __amdgpu_buffer_rsrc_t rs = make_rsrc((const void *)sb, nrec);
-        const uint32_t lead = epi.lead(p0 + q, uint32_t(reinterpret_cast<uintptr_t>((const void *)sb)) + qoff, len, kFrame);
+        const uint32_t lead = (DIAG & 64) ? kFrame - len
+                                          : epi.lead(p0 + q, uint32_t(reinterpret_cast<uintptr_t>((const void *)sb)) + qoff, len, kFrame);
         R.lead = lead;
         const uint32_t fo = qoff - lead + j * 16u;
 #pragma unroll
@@ -528,7 +523,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
                 o = (rel >= 0 && rel < int32_t(len)) ? o : 0x80000000u;
             }
             if (i == 0)
-                R.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(o), 0, 0));
+                R.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(o), 0, (DIAG & 32) ? BEpi::kLoadAux : 0));
             else
                 R.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(o), 0, BEpi::kLoadAux));
         }
@@ -560,7 +555,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         const uint64_t rr = rfirst + uint64_t(lane >> 3) * rstep;
         const uint64_t p = rr * 4 + ((lane >> 1) & 3u);
         const uint32_t st = uint32_t(reinterpret_cast<uintptr_t>(base)) + uint32_t(p) * stride;
-        const uint32_t t = (kFrame - len - epi.lead(p, st, len, kFrame)) >> 4;
+        const uint32_t t = (kFrame - len - ((DIAG & 64) ? kFrame - len : epi.lead(p, st, len, kFrame))) >> 4;
         const uint32_t tmax = (kFrame - len) >> 4;  // wave-uniform
         for (uint32_t s2 = 0; s2 < tmax; ++s2) {
             const uint32_t y = stag_apply3<0>(lds, K.kB, K.sel, acc);  // x^-128
@@ -571,7 +566,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
         const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
-        epi.put(p, acc, on, pre);
+        if (!(DIAG & 16)) epi.put(p, acc, on, pre);
         if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
@@ -658,25 +653,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // waves per CU +0.9% sustained (kbench x4, profiles/r01i/kbench_512_prio.log; it lost
     // 1% at 16 waves).  DIAG bit2 turns it off for ablations.
     uint32_t prio_round = wave >> 2;
-#ifdef WTP_AB_BUILD
-    uint32_t it = 0;  // iterations this wave has hashed (DIAG bit3 pacing)
-    const uint32_t nwaves_all = gridDim.x * nwave;
-    auto pace = [&]() {
-        if ((it & 7u) || it == 0) return;
-        const uint32_t blk = (it >> 3) - 1;  // just finished
-        if (lane == 0 && blk < 1024) atomicAdd(&g_drift[blk], 1u);
-        if (blk + 1 >= WTP_DRIFT_LAG && blk + 1 - WTP_DRIFT_LAG < 1024) {
-            const uint32_t *c = &g_drift[blk + 1 - WTP_DRIFT_LAG];
-            for (int budget = 2000; budget > 0; --budget) {
-                if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwaves_all) break;
-                __builtin_amdgcn_s_sleep(4);
-            }
-        }
-    };
-#define BR_PACE() do { if (DIAG & 8) pace(); it += 1; } while (0)
-#else
-#define BR_PACE() do { } while (0)
-#endif
     if constexpr (BEpi::kDepth == 3) {
         // three register sets, two rounds in flight while one is hashed (the fused
         // builder: only 2 waves per CU, so each wave keeps more bytes in flight)
@@ -699,19 +675,16 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     } else {
         while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
-            BR_PACE();
             load_round(r + rstep, B);
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
             r += rstep;
             if (r >= rounds) break;
-            BR_PACE();
             load_round(r + rstep, A);
             crc_round(r, B);
             r += rstep;
         }
     }
-#undef BR_PACE
     if (k) flush(0, false);
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);

@@ -237,16 +237,16 @@ int main(int argc, char **argv) {
     const unsigned grid512 = unsigned(std::min<uint64_t>((rounds + 7) / 8, s.cus));
 #define BD5(NAME, DIAG) vs.push_back({NAME, [&] { hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
     BD5("braid512_noprio", 4); BD5("braid512_prod", 0); BD5("braid512_nolut", 1); BD5("braid512_nofold", 2); BD5("braid512_skel", 3);
-    // grid pacing (DIAG bit3): its counters are zeroed before every launch, so
-    // the control variant pays the same memset
-    void *drift = nullptr;
-    CK(hipGetSymbolAddress(&drift, HIP_SYMBOL(g_drift)));
-#define BDM(NAME, DIAG) vs.push_back({NAME, [&] { (void)hipMemsetAsync(drift, 0, 4096, 0); hipLaunchKernelGGL((k_fixed_braid<6, DIAG>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, CrcBEpi{out, cinit}, s.tabs); }, {}})
-    BDM("braid512_ms", 0); BDM("varbraid512_pace", 8); BDM("braid512_skel_ms", 3); BDM("braid512_skel_pace", 11);
+    // access-pattern ablations of the skeleton: no result stores (16), row 0
+    // nt (32), right-aligned frames (64)
+    BD5("braid512_skel_nost", 3 | 16); BD5("braid512_skel_nt0", 3 | 32); BD5("braid512_skel_ra", 3 | 64);
+    BD5("braid512_skel_noprio", 3 | 4); BD5("braid512_skel_all", 3 | 16 | 32 | 64); BD5("varbraid512_ra", 64);
+    BD5("braid512_nost", 16);
     vs.push_back({"read_probe_g256x512", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(512), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
     vs.push_back({"strided_nt_d1", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 1>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_nt_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_plain_d2", [&] { hipLaunchKernelGGL((k_strided_probe<6, false, 2>), dim3(grid), dim3(1024), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
+    vs.push_back({"strided_nt_d2_g256x512", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(s.cus), dim3(512), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"strided_nt_d2_g512", [&] { hipLaunchKernelGGL((k_strided_probe<6, true, 2>), dim3(512), dim3(512), 0, 0, buf, 1456ull, 1456u, n, out); }, {}});
     vs.push_back({"g64_d2", [&] { hipLaunchKernelGGL((k_g64_probe<2>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
     vs.push_back({"g64_d4", [&] { hipLaunchKernelGGL((k_g64_probe<4>), dim3(s.cus), dim3(1024), 0, 0, buf, n, out); }, {}});
