@@ -470,7 +470,8 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
 // XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation;
 // access-pattern ablations: bit4 drops the result stores, bit5 loads row 0
-// nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len).
+// nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len), bit7
+// gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes).
 // Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
@@ -496,6 +497,9 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // every size, DESIGN 7.10, as was a translation-prefetch wave; code in git history,
     // commits f56e6d4 and 8c994a0.)
     const uint64_t rstep = uint64_t(gridDim.x) * nwave;
+    constexpr bool kB8 = (DIAG & 128) != 0;
+    const uint64_t rowstep = kB8 ? 1 : rstep;  // rounds between consecutive slot rows
+    auto nxt = [&](uint64_t x) -> uint64_t { return kB8 ? ((x & 7u) != 7u ? x + 1 : x + 8 * rstep - 7) : x + rstep; };
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -534,7 +538,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     uint64_t rfirst = 0;       // round of slot row 0
     typename BEpi::Pre pre{};  // epilogue loads for the current group
     uint32_t nfix = 0;         // datagrams this wave left to the fix-up phase (verify)
-    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rstep) * 4 + ((lane >> 1) & 3u); };
+    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rowstep) * 4 + ((lane >> 1) & 3u); };
 
     auto flush = [&](uint64_t next_g0, bool more) {
         __builtin_amdgcn_wave_barrier();
@@ -552,7 +556,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
             const uint32_t y = stag_apply3<128>(lds, K.kB, K.sel, acc);  // x^-1024
             acc = h ? y : acc;
         }
-        const uint64_t rr = rfirst + uint64_t(lane >> 3) * rstep;
+        const uint64_t rr = rfirst + uint64_t(lane >> 3) * rowstep;
         const uint64_t p = rr * 4 + ((lane >> 1) & 3u);
         const uint32_t st = uint32_t(reinterpret_cast<uintptr_t>(base)) + uint32_t(p) * stride;
         const uint32_t t = (kFrame - len - ((DIAG & 64) ? kFrame - len : epi.lead(p, st, len, kFrame))) >> 4;
@@ -611,10 +615,10 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         }
         if (k == 0) rfirst = rr;
         *(__attribute__((address_space(3))) uint32_t *)(xs + k * 256u + lane * 4u) = v;
-        if (++k == kGroup) flush(rr + rstep, true);
+        if (++k == kGroup) flush(nxt(rr), true);
     };
 
-    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
+    uint64_t r = (uint64_t(blockIdx.x) * nwave + wave) * (kB8 ? 8u : 1u);
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
@@ -675,14 +679,14 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     } else {
         while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
-            load_round(r + rstep, B);
+            load_round(nxt(r), B);
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
-            r += rstep;
+            r = nxt(r);
             if (r >= rounds) break;
-            load_round(r + rstep, A);
+            load_round(nxt(r), A);
             crc_round(r, B);
-            r += rstep;
+            r = nxt(r);
         }
     }
     if (k) flush(0, false);
