@@ -471,7 +471,9 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation;
 // access-pattern ablations: bit4 drops the result stores, bit5 loads row 0
 // nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len), bit7
-// gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes).
+// gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes),
+// bit8 stages the CRC results of a workgroup's 8 waves in an LDS ring and stores them as
+// whole 128-B lines (see stage_put below).
 // Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
@@ -538,6 +540,55 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     uint64_t rfirst = 0;       // round of slot row 0
     typename BEpi::Pre pre{};  // epilogue loads for the current group
     uint32_t nfix = 0;         // datagrams this wave left to the fix-up phase (verify)
+    // Result staging (DIAG bit8, CrcBEpi at 8 waves): flush g of every wave covers the same
+    // iterations 8g .. 8g+7, and for one iteration the workgroup's 8 waves hold rounds
+    // 8b .. 8b+7, i.e. 32 consecutive packets = one 128-B line of results.  Each wave writes
+    // its results of flush g into ring slot g % 8 ([row][4 wave + q]), counts itself in, and
+    // the eighth wave to arrive stores the slot as 8 full lines (one dwordx4 store per lane)
+    // and frees it.  A wave that is 8 flushes ahead waits for its slot (bounded spin).
+    constexpr bool kStage = (DIAG & 256) && !BEpi::kCopy && !BEpi::kFixup;
+    constexpr uint32_t kRing = kBraidXpose + 8 * 2048, kRingCtl = kRing + 8 * 1024;
+    uint32_t gidx = 0;  // flushes done by this wave
+    auto stage_put = [&](uint32_t g, uint64_t grf, uint32_t val, uint32_t row, uint32_t qq, bool on) {
+        typedef __attribute__((address_space(3))) uint32_t lu32s;
+        lu32s *const ring = (lu32s *)(lds + kRing);
+        lu32s *const ctl = (lu32s *)(lds + kRingCtl);  // [s] arrivals, [8 + s] groups done in slot s
+        const uint32_t sl = g & 7u;
+        if (g >= 8) {
+            for (uint32_t budget = 1u << 20; budget; --budget) {
+                if (*(volatile lu32s *)(ctl + 8 + sl) >= (g >> 3)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (on) ring[sl * 256u + row * 32u + 4u * wave + qq] = val;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the writes are in the ring
+        uint32_t arr = 0;
+        if (lane == 0) arr = __hip_atomic_fetch_add(ctl + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        arr = __builtin_amdgcn_readfirstlane(arr);
+        if (arr == 7u) {
+            if constexpr (kStage) {
+                const uint32_t seg = lane >> 3, part = lane & 7u;
+                const u32x4 v = *(const lu32x4 *)(ring + sl * 256u + seg * 32u + part * 4u);
+                // segment seg: iteration 8g + seg, rounds 8b .. 8b+7 (grf = this group's
+                // round of wave 0's row 0)
+                const uint64_t pb = 4 * (grf + uint64_t(seg) * rstep) + 4u * part;
+                const __amdgpu_buffer_rsrc_t ors = make_rsrc(epi.out, uint32_t(4 * n));
+                if (__builtin_amdgcn_ballot_w64(pb + 4 > n) == 0) {
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, int(4 * pb), 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(v.x, ors, pb + 0 < n ? int(4 * pb) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.y, ors, pb + 1 < n ? int(4 * pb + 4) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.z, ors, pb + 2 < n ? int(4 * pb + 8) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.w, ors, pb + 3 < n ? int(4 * pb + 12) : int(0x80000000u), 0, 0);
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring reads are done before the slot is freed
+                if (lane == 0) {
+                    ctl[sl] = 0u;
+                    ctl[8 + sl] = ctl[8 + sl] + 1u;
+                }
+            }
+        }
+    };
     auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rowstep) * 4 + ((lane >> 1) & 3u); };
 
     auto flush = [&](uint64_t next_g0, bool more) {
@@ -570,7 +621,12 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
         const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
-        if (!(DIAG & 16)) epi.put(p, acc, on, pre);
+        if constexpr (kStage) {
+            stage_put(gidx, rfirst - wave, acc ^ epi.cinit, lane >> 3, (lane >> 1) & 3u, on);
+        } else if (!(DIAG & 16)) {
+            epi.put(p, acc, on, pre);
+        }
+        ++gidx;
         if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
@@ -646,6 +702,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         for (int q2 = 0; q2 < 4; ++q2) fill_stag(lds, sets[q2].off >> 16, (sets[q2].off >> 7) & 1u, sets[q2].g);
     }
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
+    if (kStage && threadIdx.x < 16) reinterpret_cast<uint32_t *>(lds + kRingCtl)[threadIdx.x] = 0;
     __syncthreads();
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
 
@@ -690,6 +747,14 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         }
     }
     if (k) flush(0, false);
+    if constexpr (kStage) {
+        // a wave with one iteration fewer than wave 0 has no rows in the workgroup's last
+        // group: it still counts itself in (its entries are packets >= n)
+        const uint64_t r0 = uint64_t(blockIdx.x) * 8u;
+        const uint64_t it0 = r0 < rounds ? (rounds - r0 + rstep - 1) / rstep : 0;
+        const uint32_t groups = uint32_t((it0 + 7) / 8);
+        if (nwave == 8 && gidx < groups) stage_put(groups - 1, r0 + 8 * uint64_t(groups - 1) * rstep, 0u, 0u, 0u, false);
+    }
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);
 }
