@@ -473,7 +473,9 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len), bit7
 // gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes),
 // bit8 stages the CRC results of a workgroup's 8 waves in an LDS ring and stores them as
-// whole 128-B lines (see stage_put below).
+// whole 128-B lines (see stage_put below), bit9 defers a group's flush until the next
+// round's loads are issued (its result store then queues behind them), bit10 keeps a wave's
+// results of 16 flushes (128 rounds) in LDS and stores them in one burst (dump below).
 // Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
@@ -549,6 +551,36 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     constexpr bool kStage = (DIAG & 256) && !BEpi::kCopy && !BEpi::kFixup;
     constexpr uint32_t kRing = kBraidXpose + 8 * 2048, kRingCtl = kRing + 8 * 1024;
     uint32_t gidx = 0;  // flushes done by this wave
+    uint64_t late = ~0ull;  // DIAG bit9: the deferred flush's next group round
+    // DIAG bit10: per-wave result buffer, 16 flushes x 32 results (2 KiB at slot 8 + wave)
+    constexpr bool kDump = (DIAG & 1024) && !BEpi::kCopy && !BEpi::kFixup;
+    lchar *const rbuf = (lchar *)(lds + kBraidXpose + (8u + wave) * 2048u);
+    uint32_t dgroups = 0;    // flushes held in rbuf
+    uint64_t dfirst = 0;     // round of the first held flush's row 0 (this wave)
+    auto dump = [&]() {
+        if constexpr (kDump) {
+            __builtin_amdgcn_wave_barrier();
+            const __amdgpu_buffer_rsrc_t ors = make_rsrc(epi.out, uint32_t(4 * n));
+#pragma unroll
+            for (uint32_t t = 0; t < 2; ++t) {
+                const uint32_t si = lane + 64u * t;  // segment: flush si >> 3, row si & 7
+                const u32x4 v = *(const lu32x4 *)(rbuf + si * 16u);
+                const uint64_t rr = dfirst + (8u * uint64_t(si >> 3) + (si & 7u)) * rstep;
+                const uint64_t pb = 4 * rr;
+                const bool live = (si >> 3) < dgroups && rr < rounds;
+                if (__builtin_amdgcn_ballot_w64(live && pb + 4 > n) == 0) {
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, live ? int(4 * pb) : int(0x80000000u), 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(v.x, ors, live && pb + 0 < n ? int(4 * pb) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.y, ors, live && pb + 1 < n ? int(4 * pb + 4) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.z, ors, live && pb + 2 < n ? int(4 * pb + 8) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.w, ors, live && pb + 3 < n ? int(4 * pb + 12) : int(0x80000000u), 0, 0);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            dgroups = 0;
+        }
+    };
     auto stage_put = [&](uint32_t g, uint64_t grf, uint32_t val, uint32_t row, uint32_t qq, bool on) {
         typedef __attribute__((address_space(3))) uint32_t lu32s;
         lu32s *const ring = (lu32s *)(lds + kRing);
@@ -623,6 +655,11 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
         if constexpr (kStage) {
             stage_put(gidx, rfirst - wave, acc ^ epi.cinit, lane >> 3, (lane >> 1) & 3u, on);
+        } else if constexpr (kDump) {
+            if (dgroups == 0) dfirst = rfirst;
+            // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
+            if (h == 0) *(__attribute__((address_space(3))) uint32_t *)(rbuf + (dgroups * 8u + (lane >> 3)) * 16u + ((lane >> 1) & 3u) * 4u) = acc ^ epi.cinit;
+            if (++dgroups == 16) dump();
         } else if (!(DIAG & 16)) {
             epi.put(p, acc, on, pre);
         }
@@ -671,7 +708,13 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         }
         if (k == 0) rfirst = rr;
         *(__attribute__((address_space(3))) uint32_t *)(xs + k * 256u + lane * 4u) = v;
-        if (++k == kGroup) flush(nxt(rr), true);
+        if (++k == kGroup) {
+            if constexpr ((DIAG & 512) != 0) {
+                late = nxt(rr);
+            } else {
+                flush(nxt(rr), true);
+            }
+        }
     };
 
     uint64_t r = (uint64_t(blockIdx.x) * nwave + wave) * (kB8 ? 8u : 1u);
@@ -737,16 +780,28 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
             load_round(nxt(r), B);
+            if ((DIAG & 512) && late != ~0ull) {
+                flush(late, true);
+                late = ~0ull;
+            }
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
             r = nxt(r);
             if (r >= rounds) break;
             load_round(nxt(r), A);
+            if ((DIAG & 512) && late != ~0ull) {
+                flush(late, true);
+                late = ~0ull;
+            }
             crc_round(r, B);
             r = nxt(r);
         }
     }
+    if ((DIAG & 512) && late != ~0ull) flush(late, false);  // k == 8, nothing more after it
     if (k) flush(0, false);
+    if constexpr (kDump) {
+        if (dgroups) dump();
+    }
     if constexpr (kStage) {
         // a wave with one iteration fewer than wave 0 has no rows in the workgroup's last
         // group: it still counts itself in (its entries are packets >= n)
