@@ -287,6 +287,7 @@ struct CrcBEpi {  // out[p] = crc
     static constexpr int kDiag = 0;       // DIAG of the production instantiation
     static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     static constexpr int kLoadAux = 2;   // rows >= 1 stream (nt); row 0 is temporal (see k_fixed_braid)
+    static constexpr bool kHold = true;  // results held in LDS, stored in bursts (k_fixed_braid)
     __device__ __forceinline__ uint32_t lead(uint64_t, uint32_t st, uint32_t len, uint32_t frame) const {
         return braid_lead(st, len, frame);
     }
@@ -308,6 +309,7 @@ struct CrcBEpi {  // out[p] = crc
 // fix-up phase (verify_fixup, after its braided rounds) recomputes it with the
 // reference's semantics: one launch, no state outside the caller's buffers.
 struct VerifyBEpi {
+    static constexpr bool kHold = false;  // see CrcBEpi
     static constexpr bool kCopy = false;
     static constexpr bool kFixup = true;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // verify_fixup's LDS layout assumes 8 waves
@@ -376,6 +378,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 #define WTP_BUILD_SAUX0 0  // the same for row 0 (it shares a 64-B segment with the header)
 #endif
 struct BuildBEpi {
+    static constexpr bool kHold = false;  // see CrcBEpi
     static constexpr bool kCopy = true;
     static constexpr bool kFixup = false;  // see VerifyBEpi
     // launched at 128 threads: the bound lets the copy rows keep their registers (at the
@@ -474,8 +477,9 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes),
 // bit8 stages the CRC results of a workgroup's 8 waves in an LDS ring and stores them as
 // whole 128-B lines (see stage_put below), bit9 defers a group's flush until the next
-// round's loads are issued (its result store then queues behind them), bit10 keeps a wave's
-// results of 16 flushes (128 rounds) in LDS and stores them in one burst (dump below).
+// round's loads are issued (its result store then queues behind them), bit10 holds the
+// results in LDS for any epilogue (CrcBEpi does by default, see kDump), bit11 turns that off
+// (one result store per flush, the round-3 form).
 // Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
@@ -552,8 +556,16 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     constexpr uint32_t kRing = kBraidXpose + 8 * 2048, kRingCtl = kRing + 8 * 1024;
     uint32_t gidx = 0;  // flushes done by this wave
     uint64_t late = ~0ull;  // DIAG bit9: the deferred flush's next group round
-    // DIAG bit10: per-wave result buffer, 16 flushes x 32 results (2 KiB at slot 8 + wave)
-    constexpr bool kDump = (DIAG & 1024) && !BEpi::kCopy && !BEpi::kFixup;
+    // Results (CrcBEpi): a flush writes its 32 CRCs into the wave's LDS result buffer (2 KiB
+    // at transposition slot 8 + wave, free at 8 waves) instead of storing them, and every
+    // 16 flushes (128 rounds) the wave stores the buffer in one burst of two dwordx4 stores
+    // per lane.  A 1 M batch then writes its 4 MiB of results near the end of the launch
+    // instead of 32 B per wave every 8 rounds among the reads: 1 M x 1456 B alternating
+    // between two buffers 232.8 -> 225.9 us, same buffer 221.9 -> 220.5 us (interleaved
+    // kbench, profiles/r04r; no stores at all: 221.7 / 219.1).  Waiting for the store acks
+    // was not it (deferring the flush past the next loads: neutral, profiles/r04q), nor
+    // partial lines (whole-line stores per wave: neutral, profiles/r04o).
+    constexpr bool kDump = ((BEpi::kHold && !(DIAG & 2048)) || (DIAG & 1024)) && !BEpi::kCopy && !BEpi::kFixup;
     lchar *const rbuf = (lchar *)(lds + kBraidXpose + (8u + wave) * 2048u);
     uint32_t dgroups = 0;    // flushes held in rbuf
     uint64_t dfirst = 0;     // round of the first held flush's row 0 (this wave)
@@ -656,10 +668,16 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if constexpr (kStage) {
             stage_put(gidx, rfirst - wave, acc ^ epi.cinit, lane >> 3, (lane >> 1) & 3u, on);
         } else if constexpr (kDump) {
-            if (dgroups == 0) dfirst = rfirst;
-            // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
-            if (h == 0) *(__attribute__((address_space(3))) uint32_t *)(rbuf + (dgroups * 8u + (lane >> 3)) * 16u + ((lane >> 1) & 3u) * 4u) = acc ^ epi.cinit;
-            if (++dgroups == 16) dump();
+            if (nwave <= 8) {  // the buffer sits in the transposition slots of waves 8..15
+                if (dgroups == 0) dfirst = rfirst;
+                // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
+                if (h == 0)
+                    *(__attribute__((address_space(3))) uint32_t *)(rbuf + (dgroups * 8u + (lane >> 3)) * 16u +
+                                                                     ((lane >> 1) & 3u) * 4u) = acc ^ epi.cinit;
+                if (++dgroups == 16) dump();
+            } else if (!(DIAG & 16)) {
+                epi.put(p, acc, on, pre);
+            }
         } else if (!(DIAG & 16)) {
             epi.put(p, acc, on, pre);
         }
