@@ -566,6 +566,10 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // was not it (deferring the flush past the next loads: neutral, profiles/r04q), nor
     // partial lines (whole-line stores per wave: neutral, profiles/r04o).
     constexpr bool kDump = ((BEpi::kHold && !(DIAG & 2048)) || (DIAG & 1024)) && !BEpi::kCopy && !BEpi::kFixup;
+    // Short batches store directly: with a few rounds per wave the burst would only lengthen
+    // the tail (C2, 64 K packets, 8 rounds per wave: 15.48 -> 15.73 us from a graph).  Held
+    // from 64 rounds per wave on, the long-batch rule of the launcher's grid.
+    const bool hold = kDump && nwave <= 8 && rounds >= 64 * rstep;
     lchar *const rbuf = (lchar *)(lds + kBraidXpose + (8u + wave) * 2048u);
     uint32_t dgroups = 0;    // flushes held in rbuf
     uint64_t dfirst = 0;     // round of the first held flush's row 0 (this wave)
@@ -668,7 +672,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         if constexpr (kStage) {
             stage_put(gidx, rfirst - wave, acc ^ epi.cinit, lane >> 3, (lane >> 1) & 3u, on);
         } else if constexpr (kDump) {
-            if (nwave <= 8) {  // the buffer sits in the transposition slots of waves 8..15
+            if (hold) {  // the buffer sits in the transposition slots of waves 8..15
                 if (dgroups == 0) dfirst = rfirst;
                 // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
                 if (h == 0)
