@@ -287,7 +287,7 @@ struct CrcBEpi {  // out[p] = crc
     static constexpr int kDiag = 0;       // DIAG of the production instantiation
     static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     static constexpr int kLoadAux = 2;   // rows >= 1 stream (nt); row 0 is temporal (see k_fixed_braid)
-    static constexpr bool kHold = true;  // results held in LDS, stored in bursts (k_fixed_braid)
+    static constexpr bool kHold = false;  // CrcHoldBEpi: results held in LDS, stored in bursts
     __device__ __forceinline__ uint32_t lead(uint64_t, uint32_t st, uint32_t len, uint32_t frame) const {
         return braid_lead(st, len, frame);
     }
@@ -299,6 +299,11 @@ struct CrcBEpi {  // out[p] = crc
     __device__ __forceinline__ void put(uint64_t p, uint32_t v, bool on, const Pre &) const {
         if (on) out[p] = v ^ cinit;
     }
+};
+// The same epilogue for long batches (the launcher's rule): k_fixed_braid holds the CRCs in
+// LDS and stores them in bursts (see kDump there).
+struct CrcHoldBEpi : CrcBEpi {
+    static constexpr bool kHold = true;
 };
 // Receiver verify over a datagram ring: the kernel runs on base = ring + 16 with the
 // ring's "full" payload length len (1456 for a WTP ring: 1472-B datagrams, whatever the
@@ -478,8 +483,8 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // bit8 stages the CRC results of a workgroup's 8 waves in an LDS ring and stores them as
 // whole 128-B lines (see stage_put below), bit9 defers a group's flush until the next
 // round's loads are issued (its result store then queues behind them), bit10 holds the
-// results in LDS for any epilogue (CrcBEpi does by default, see kDump), bit11 turns that off
-// (one result store per flush, the round-3 form).
+// results in LDS for any CRC epilogue (CrcHoldBEpi does without it, see kDump), bit11 turns
+// that off (one result store per flush).
 // Production instantiations use DIAG = 0.
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
@@ -556,7 +561,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     constexpr uint32_t kRing = kBraidXpose + 8 * 2048, kRingCtl = kRing + 8 * 1024;
     uint32_t gidx = 0;  // flushes done by this wave
     uint64_t late = ~0ull;  // DIAG bit9: the deferred flush's next group round
-    // Results (CrcBEpi): a flush writes its 32 CRCs into the wave's LDS result buffer (2 KiB
+    // Results (CrcHoldBEpi): a flush writes its 32 CRCs into the wave's LDS result buffer (2 KiB
     // at transposition slot 8 + wave, free at 8 waves) instead of storing them, and every
     // 16 flushes (128 rounds) the wave stores the buffer in one burst of two dwordx4 stores
     // per lane.  A 1 M batch then writes its 4 MiB of results near the end of the launch
@@ -566,10 +571,13 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // was not it (deferring the flush past the next loads: neutral, profiles/r04q), nor
     // partial lines (whole-line stores per wave: neutral, profiles/r04o).
     constexpr bool kDump = ((BEpi::kHold && !(DIAG & 2048)) || (DIAG & 1024)) && !BEpi::kCopy && !BEpi::kFixup;
-    // Short batches store directly: with a few rounds per wave the burst would only lengthen
-    // the tail (C2, 64 K packets, 8 rounds per wave: 15.48 -> 15.73 us from a graph).  Held
-    // from 64 rounds per wave on, the long-batch rule of the launcher's grid.
-    const bool hold = kDump && nwave <= 8 && rounds >= 64 * rstep;
+    // (the launcher picks CrcHoldBEpi for long batches only; the buffer needs 8 waves)
+    const bool hold = kDump && nwave <= 8;
+#ifndef WTP_BR_HOLD
+#define WTP_BR_HOLD 16  // flushes held per burst (A/B builds: 4, 8)
+#endif
+    constexpr uint32_t kHoldG = WTP_BR_HOLD;
+    static_assert(kHoldG == 4 || kHoldG == 8 || kHoldG == 16, "hold capacity");
     lchar *const rbuf = (lchar *)(lds + kBraidXpose + (8u + wave) * 2048u);
     uint32_t dgroups = 0;    // flushes held in rbuf
     uint64_t dfirst = 0;     // round of the first held flush's row 0 (this wave)
@@ -578,7 +586,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
             __builtin_amdgcn_wave_barrier();
             const __amdgpu_buffer_rsrc_t ors = make_rsrc(epi.out, uint32_t(4 * n));
 #pragma unroll
-            for (uint32_t t = 0; t < 2; ++t) {
+            for (uint32_t t = 0; t < (kHoldG * 8 + 63) / 64; ++t) {
                 const uint32_t si = lane + 64u * t;  // segment: flush si >> 3, row si & 7
                 const u32x4 v = *(const lu32x4 *)(rbuf + si * 16u);
                 const uint64_t rr = dfirst + (8u * uint64_t(si >> 3) + (si & 7u)) * rstep;
@@ -678,7 +686,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
                 if (h == 0)
                     *(__attribute__((address_space(3))) uint32_t *)(rbuf + (dgroups * 8u + (lane >> 3)) * 16u +
                                                                      ((lane >> 1) & 3u) * 4u) = acc ^ epi.cinit;
-                if (++dgroups == 16) dump();
+                if (++dgroups == kHoldG) dump();
             } else if (!(DIAG & 16)) {
                 epi.put(p, acc, on, pre);
             }
@@ -2119,6 +2127,13 @@ void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_
 // Braided kernel over n packets base[p*stride, +len): base, stride, len multiples of 16,
 // 16 <= len <= 1536, stride <= 16 KiB.  The epilogue's cinit is filled in here.
 template <class BEpi>
+int launch_fixed_braid_rows(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
+                            hipStream_t st, unsigned grid, unsigned threads, int rows);
+#ifndef WTP_BR_HOLD_ROUNDS
+#define WTP_BR_HOLD_ROUNDS 64  // rounds per wave from which the CRC holds its results (CrcHoldBEpi)
+#endif
+
+template <class BEpi>
 int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
                        hipStream_t st) {
     const int rows = int((len + 255) / 256);
@@ -2135,6 +2150,22 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
         cap -= cap / 32;
     const unsigned grid = unsigned(want < cap ? want : cap);
     epi.cinit = init_const(len);
+    if constexpr (std::is_same_v<BEpi, dev::CrcBEpi>) {
+        // long batches hold their results in LDS (k_fixed_braid, kDump): short ones store
+        // directly, the held form's code was 1.4-1.7% slower on 16 K-64 K packets even with
+        // nothing held (profiles/r04u)
+        if (rounds >= uint64_t(WTP_BR_HOLD_ROUNDS) * grid * (threads / 64)) {
+            dev::CrcHoldBEpi h;
+            static_cast<dev::CrcBEpi &>(h) = epi;
+            return launch_fixed_braid_rows(s, base, stride, len, n, h, st, grid, threads, rows);
+        }
+    }
+    return launch_fixed_braid_rows(s, base, stride, len, n, epi, st, grid, threads, rows);
+}
+
+template <class BEpi>
+int launch_fixed_braid_rows(DevState &s, const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, BEpi epi,
+                            hipStream_t st, unsigned grid, unsigned threads, int rows) {
     switch (rows) {
         case 1: launch_braid_rows<1>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
         case 2: launch_braid_rows<2>(grid, threads, st, base, stride, len, n, epi, s.tabs); break;
