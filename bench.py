@@ -689,7 +689,7 @@ def main():
                    "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,
-                     "kernel": "k_fixed_braid<6>", "kernel_ms_mean": round(kmean, 5),
+                     "kernel": "k_fixed_braid<6, 0, CrcHoldBEpi>", "kernel_ms_mean": round(kmean, 5),
                      "kernel_ms_median": round(kern_ms[len(kern_ms) // 2], 5),
                      "kernel_ms_p10": round(kern_ms[len(kern_ms) // 10], 5),
                      "kernel_ms_p90": round(kern_ms[(9 * len(kern_ms)) // 10], 5),

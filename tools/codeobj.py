@@ -92,8 +92,9 @@ def kernel_code_sha256(lib_path: str, pattern: str) -> dict:
     return {"kernel": hits[0], "code_bytes": size, "sha256": hashlib.sha256(co[off:off + size]).hexdigest()}
 
 
-# the headline kernel: k_fixed_braid<6 rows, DIAG 0, CrcBEpi> (1456-B payloads)
-HEADLINE_KERNEL = r"k_fixed_braidILi6ELi0ENS0_7CrcBEpiE"
+# the headline kernel: k_fixed_braid<6 rows, DIAG 0, CrcHoldBEpi> (1456-B payloads; the
+# launcher's long-batch epilogue, which 1 M packets use)
+HEADLINE_KERNEL = r"k_fixed_braidILi6ELi0ENS0_11CrcHoldBEpiE"
 
 if __name__ == "__main__":
     import json
