@@ -478,14 +478,11 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
 // XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation;
 // access-pattern ablations: bit4 drops the result stores, bit5 loads row 0
-// nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len), bit7
-// gives each wave blocks of 8 consecutive rounds (a flush then stores 128 contiguous bytes),
-// bit8 stages the CRC results of a workgroup's 8 waves in an LDS ring and stores them as
-// whole 128-B lines (see stage_put below), bit9 defers a group's flush until the next
-// round's loads are issued (its result store then queues behind them), bit10 holds the
-// results in LDS for any CRC epilogue (CrcHoldBEpi does without it, see kDump), bit11 turns
-// that off (one result store per flush).
-// Production instantiations use DIAG = 0.
+// nt as well, bit6 right-aligns every frame to its packet end (lead = frame - len), bit10
+// holds the results in LDS for any CRC epilogue (CrcHoldBEpi does without it, see kDump),
+// bit11 turns that off.  Production instantiations use DIAG = 0.  (Rejected round-4 forms,
+// in git history at commit ba1b383: blocked-8 round order, a workgroup result ring, a
+// deferred flush.)
 template <int ROWS, int DIAG = 0, class BEpi = CrcBEpi>
 __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__restrict__ base, uint32_t stride,
                                                       uint32_t len, uint64_t n, BEpi epi,
@@ -510,9 +507,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     // every size, DESIGN 7.10, as was a translation-prefetch wave; code in git history,
     // commits f56e6d4 and 8c994a0.)
     const uint64_t rstep = uint64_t(gridDim.x) * nwave;
-    constexpr bool kB8 = (DIAG & 128) != 0;
-    const uint64_t rowstep = kB8 ? 1 : rstep;  // rounds between consecutive slot rows
-    auto nxt = [&](uint64_t x) -> uint64_t { return kB8 ? ((x & 7u) != 7u ? x + 1 : x + 8 * rstep - 7) : x + rstep; };
     const uint32_t qoff = q * stride;
     gu8 *const gbase = (gu8 *)base;
 
@@ -551,16 +545,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     uint64_t rfirst = 0;       // round of slot row 0
     typename BEpi::Pre pre{};  // epilogue loads for the current group
     uint32_t nfix = 0;         // datagrams this wave left to the fix-up phase (verify)
-    // Result staging (DIAG bit8, CrcBEpi at 8 waves): flush g of every wave covers the same
-    // iterations 8g .. 8g+7, and for one iteration the workgroup's 8 waves hold rounds
-    // 8b .. 8b+7, i.e. 32 consecutive packets = one 128-B line of results.  Each wave writes
-    // its results of flush g into ring slot g % 8 ([row][4 wave + q]), counts itself in, and
-    // the eighth wave to arrive stores the slot as 8 full lines (one dwordx4 store per lane)
-    // and frees it.  A wave that is 8 flushes ahead waits for its slot (bounded spin).
-    constexpr bool kStage = (DIAG & 256) && !BEpi::kCopy && !BEpi::kFixup;
-    constexpr uint32_t kRing = kBraidXpose + 8 * 2048, kRingCtl = kRing + 8 * 1024;
-    uint32_t gidx = 0;  // flushes done by this wave
-    uint64_t late = ~0ull;  // DIAG bit9: the deferred flush's next group round
     // Results (CrcHoldBEpi): a flush writes its 32 CRCs into the wave's LDS result buffer (2 KiB
     // at transposition slot 8 + wave, free at 8 waves) instead of storing them, and every
     // 16 flushes (128 rounds) the wave stores the buffer in one burst of two dwordx4 stores
@@ -605,47 +589,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
             dgroups = 0;
         }
     };
-    auto stage_put = [&](uint32_t g, uint64_t grf, uint32_t val, uint32_t row, uint32_t qq, bool on) {
-        typedef __attribute__((address_space(3))) uint32_t lu32s;
-        lu32s *const ring = (lu32s *)(lds + kRing);
-        lu32s *const ctl = (lu32s *)(lds + kRingCtl);  // [s] arrivals, [8 + s] groups done in slot s
-        const uint32_t sl = g & 7u;
-        if (g >= 8) {
-            for (uint32_t budget = 1u << 20; budget; --budget) {
-                if (*(volatile lu32s *)(ctl + 8 + sl) >= (g >> 3)) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        if (on) ring[sl * 256u + row * 32u + 4u * wave + qq] = val;
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the writes are in the ring
-        uint32_t arr = 0;
-        if (lane == 0) arr = __hip_atomic_fetch_add(ctl + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        arr = __builtin_amdgcn_readfirstlane(arr);
-        if (arr == 7u) {
-            if constexpr (kStage) {
-                const uint32_t seg = lane >> 3, part = lane & 7u;
-                const u32x4 v = *(const lu32x4 *)(ring + sl * 256u + seg * 32u + part * 4u);
-                // segment seg: iteration 8g + seg, rounds 8b .. 8b+7 (grf = this group's
-                // round of wave 0's row 0)
-                const uint64_t pb = 4 * (grf + uint64_t(seg) * rstep) + 4u * part;
-                const __amdgpu_buffer_rsrc_t ors = make_rsrc(epi.out, uint32_t(4 * n));
-                if (__builtin_amdgcn_ballot_w64(pb + 4 > n) == 0) {
-                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, int(4 * pb), 0, 0);
-                } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(v.x, ors, pb + 0 < n ? int(4 * pb) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.y, ors, pb + 1 < n ? int(4 * pb + 4) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.z, ors, pb + 2 < n ? int(4 * pb + 8) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.w, ors, pb + 3 < n ? int(4 * pb + 12) : int(0x80000000u), 0, 0);
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);  // the ring reads are done before the slot is freed
-                if (lane == 0) {
-                    ctl[sl] = 0u;
-                    ctl[8 + sl] = ctl[8 + sl] + 1u;
-                }
-            }
-        }
-    };
-    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rowstep) * 4 + ((lane >> 1) & 3u); };
+    auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rstep) * 4 + ((lane >> 1) & 3u); };
 
     auto flush = [&](uint64_t next_g0, bool more) {
         __builtin_amdgcn_wave_barrier();
@@ -663,7 +607,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
             const uint32_t y = stag_apply3<128>(lds, K.kB, K.sel, acc);  // x^-1024
             acc = h ? y : acc;
         }
-        const uint64_t rr = rfirst + uint64_t(lane >> 3) * rowstep;
+        const uint64_t rr = rfirst + uint64_t(lane >> 3) * rstep;
         const uint64_t p = rr * 4 + ((lane >> 1) & 3u);
         const uint32_t st = uint32_t(reinterpret_cast<uintptr_t>(base)) + uint32_t(p) * stride;
         const uint32_t t = (kFrame - len - ((DIAG & 64) ? kFrame - len : epi.lead(p, st, len, kFrame))) >> 4;
@@ -677,9 +621,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
         const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
-        if constexpr (kStage) {
-            stage_put(gidx, rfirst - wave, acc ^ epi.cinit, lane >> 3, (lane >> 1) & 3u, on);
-        } else if constexpr (kDump) {
+        if constexpr (kDump) {
             if (hold) {  // the buffer sits in the transposition slots of waves 8..15
                 if (dgroups == 0) dfirst = rfirst;
                 // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
@@ -693,7 +635,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         } else if (!(DIAG & 16)) {
             epi.put(p, acc, on, pre);
         }
-        ++gidx;
         if constexpr (BEpi::kFixup) nfix += uint32_t(__popcll(__ballot(epi.listed(on, pre))));
         if (more) epi.pre(group_packet(next_g0), pre);
         k = 0;
@@ -738,16 +679,10 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         }
         if (k == 0) rfirst = rr;
         *(__attribute__((address_space(3))) uint32_t *)(xs + k * 256u + lane * 4u) = v;
-        if (++k == kGroup) {
-            if constexpr ((DIAG & 512) != 0) {
-                late = nxt(rr);
-            } else {
-                flush(nxt(rr), true);
-            }
-        }
+        if (++k == kGroup) flush(rr + rstep, true);
     };
 
-    uint64_t r = (uint64_t(blockIdx.x) * nwave + wave) * (kB8 ? 8u : 1u);
+    uint64_t r = uint64_t(blockIdx.x) * nwave + wave;
     // the first loads are issued before the LDS table fill so the fill overlaps them
     Round A, B;
     // braid tables, x^-32 (region A); x^-128, x^-1024 (region B): their loads go out
@@ -775,7 +710,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         for (int q2 = 0; q2 < 4; ++q2) fill_stag(lds, sets[q2].off >> 16, (sets[q2].off >> 7) & 1u, sets[q2].g);
     }
     PC_PROBE(2, __builtin_amdgcn_s_memrealtime());
-    if (kStage && threadIdx.x < 16) reinterpret_cast<uint32_t *>(lds + kRingCtl)[threadIdx.x] = 0;
     __syncthreads();
     PC_PROBE(3, __builtin_amdgcn_s_memrealtime());
 
@@ -809,36 +743,19 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     } else {
         while (r < rounds) {
             if (!(DIAG & 4)) rotate_prio(++prio_round);
-            load_round(nxt(r), B);
-            if ((DIAG & 512) && late != ~0ull) {
-                flush(late, true);
-                late = ~0ull;
-            }
+            load_round(r + rstep, B);
             crc_round(r, A);
             if (WTP_PROBE && prio_round == (wave >> 2) + 1) PC_PROBE(4, __builtin_amdgcn_s_memrealtime());
-            r = nxt(r);
+            r += rstep;
             if (r >= rounds) break;
-            load_round(nxt(r), A);
-            if ((DIAG & 512) && late != ~0ull) {
-                flush(late, true);
-                late = ~0ull;
-            }
+            load_round(r + rstep, A);
             crc_round(r, B);
-            r = nxt(r);
+            r += rstep;
         }
     }
-    if ((DIAG & 512) && late != ~0ull) flush(late, false);  // k == 8, nothing more after it
     if (k) flush(0, false);
     if constexpr (kDump) {
         if (dgroups) dump();
-    }
-    if constexpr (kStage) {
-        // a wave with one iteration fewer than wave 0 has no rows in the workgroup's last
-        // group: it still counts itself in (its entries are packets >= n)
-        const uint64_t r0 = uint64_t(blockIdx.x) * 8u;
-        const uint64_t it0 = r0 < rounds ? (rounds - r0 + rstep - 1) / rstep : 0;
-        const uint32_t groups = uint32_t((it0 + 7) / 8);
-        if (nwave == 8 && gidx < groups) stage_put(groups - 1, r0 + 8 * uint64_t(groups - 1) * rstep, 0u, 0u, 0u, false);
     }
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);

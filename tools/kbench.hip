@@ -241,7 +241,7 @@ int main(int argc, char **argv) {
     // nt (32), right-aligned frames (64)
     BD5("braid512_skel_nost", 3 | 16); BD5("braid512_skel_nt0", 3 | 32); BD5("braid512_skel_ra", 3 | 64);
     BD5("braid512_skel_noprio", 3 | 4); BD5("braid512_skel_all", 3 | 16 | 32 | 64); BD5("varbraid512_ra", 64);
-    BD5("braid512_nost", 16); BD5("varbraid512_b8", 128); BD5("braid512_b8nost", 128 | 16); BD5("braid512_skel_b8", 3 | 128); BD5("varbraid512_stage", 256); BD5("braid512_skel_stage", 3 | 256); BD5("varbraid512_late", 512); BD5("varbraid512_direct", 2048); BD5("braid512_skel_hold", 3 | 1024);
+    BD5("braid512_nost", 16);  BD5("varbraid512_direct", 2048); BD5("braid512_skel_hold", 3 | 1024);
     vs.push_back({"varbraid512_hold", [&] { CrcHoldBEpi h; static_cast<CrcBEpi &>(h) = CrcBEpi{out, cinit};
         hipLaunchKernelGGL((k_fixed_braid<6, 0, CrcHoldBEpi>), dim3(grid512), dim3(512), 0, 0, buf, 1456u, 1456u, n, h, s.tabs); }, {}});
     vs.push_back({"read_probe_g256x512", [&] { hipLaunchKernelGGL(k_read_probe, dim3(s.cus), dim3(512), 0, 0, (const u32x4 *)buf, bytes / 16, out); }, {}});
