@@ -568,21 +568,26 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     auto dump = [&]() {
         if constexpr (kDump) {
             __builtin_amdgcn_wave_barrier();
-            const __amdgpu_buffer_rsrc_t ors = make_rsrc(epi.out, uint32_t(4 * n));
+            // buffer resource from this dump's first packet: its offsets stay below
+            // 16 * kHoldG * 8 * rstep (< 2^31) and the range ends at packet n for any n
+            const uint64_t pb0 = 4 * dfirst, left = n > pb0 ? n - pb0 : 0;
+            const __amdgpu_buffer_rsrc_t ors =
+                make_rsrc(epi.out + pb0, left >= (1ull << 29) ? 0x80000000u : uint32_t(4 * left));
 #pragma unroll
             for (uint32_t t = 0; t < (kHoldG * 8 + 63) / 64; ++t) {
                 const uint32_t si = lane + 64u * t;  // segment: flush si >> 3, row si & 7
                 const u32x4 v = *(const lu32x4 *)(rbuf + si * 16u);
                 const uint64_t rr = dfirst + (8u * uint64_t(si >> 3) + (si & 7u)) * rstep;
                 const uint64_t pb = 4 * rr;
+                const uint32_t o = uint32_t(4 * (pb - pb0));
                 const bool live = (si >> 3) < dgroups && rr < rounds;
                 if (__builtin_amdgcn_ballot_w64(live && pb + 4 > n) == 0) {
-                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, live ? int(4 * pb) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, live ? int(o) : int(0x80000000u), 0, 0);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(v.x, ors, live && pb + 0 < n ? int(4 * pb) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.y, ors, live && pb + 1 < n ? int(4 * pb + 4) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.z, ors, live && pb + 2 < n ? int(4 * pb + 8) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(v.w, ors, live && pb + 3 < n ? int(4 * pb + 12) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.x, ors, live && pb + 0 < n ? int(o) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.y, ors, live && pb + 1 < n ? int(o + 4) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.z, ors, live && pb + 2 < n ? int(o + 8) : int(0x80000000u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v.w, ors, live && pb + 3 < n ? int(o + 12) : int(0x80000000u), 0, 0);
                 }
             }
             __builtin_amdgcn_wave_barrier();

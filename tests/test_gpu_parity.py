@@ -66,6 +66,28 @@ def test_golden_batch_digest(W, golden):
     assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_le_u32"]
 
 
+def test_fixed_held_results_past_2g_result_bytes(W):
+    """Held results (CrcHoldBEpi, long batches) past 2^29 packets: 16-B payloads, n =
+    2^29 + 1237 (8.6 GB of payloads, 2.1 GB of results), so result byte offsets pass 2^31
+    and the last dump ends mid-segment.  Spot checks against the oracle around the 2^29
+    boundary, at the tail and at random packets."""
+    n = (1 << 29) + 1237
+    buf = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    W.crc32_batch_fixed(buf, 16, 16, n, out)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(29)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 1500), np.arange(n - 600, n),
+                                    np.arange((1 << 29) - 300, (1 << 29) + 300), np.arange(0, 64)]))
+    got = out[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32)
+    want = np.array([O.crc32(O.synth_fill_np(16, start_byte=int(i) * 16)) for i in idx], dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at packets {idx[bad[:5]]}"
+    del buf, out
+    torch.cuda.empty_cache()
+
+
 def test_reserve_cus_keeps_results(W, golden):
     """wtp_reserve_cus shrinks the persistent grids; results stay bit-exact (golden
     4096 x 1456 digest, a long batch past the 64-rounds-per-wave grid rule, and a mixed
