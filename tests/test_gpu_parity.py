@@ -88,6 +88,25 @@ def test_fixed_held_results_past_2g_result_bytes(W):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("length,stride", [(16, 16), (256, 256), (528, 544), (1024, 1024), (1296, 1312), (1536, 1536)])
+def test_fixed_held_results_every_row_count(W, length, stride):
+    """Long batches (>= 64 rounds per wave: the held-results epilogue) at every braided row
+    count 1-6, odd n (a partial last round and a partial last dump), strides above the
+    payload length: every packet of a sampled set and the whole tail against the oracle."""
+    n = 600_001
+    buf = torch.empty(n * stride + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    W.crc32_batch_fixed(buf, stride, length, n, out)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(length)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 400), np.arange(n - 300, n), np.arange(0, 40)]))
+    got = out[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32)
+    want = np.array([O.crc32(O.synth_fill_np(length, start_byte=int(i) * stride)) for i in idx], dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at packets {idx[bad[:5]]}"
+
+
 def test_reserve_cus_keeps_results(W, golden):
     """wtp_reserve_cus shrinks the persistent grids; results stay bit-exact (golden
     4096 x 1456 digest, a long batch past the 64-rounds-per-wave grid rule, and a mixed
