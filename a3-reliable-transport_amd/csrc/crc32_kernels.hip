@@ -473,7 +473,8 @@ __device__ __forceinline__ void verify_fixup(char *lds, const VerifyBEpi &epi, c
 // skeleton's (kbench + GRBM_GUI_ACTIVE, profiles/).  Every VALU/LDS instruction in the
 // loop therefore costs bandwidth: XORs are v_bitop3_b32 (3-input, new on gfx950), a
 // lookup address is one v_perm_b32 into the staggered conflict-free tables, results are
-// stored once per 8 rounds (on gfx950 stores share vmcnt with loads).
+// stored once per 8 rounds (on gfx950 stores share vmcnt with loads), and long batches
+// (CrcHoldBEpi) hold them in LDS and store them once per 128 rounds (see kDump).
 //
 // DIAG (ablation builds only, tools/kbench.hip): bit0 replaces the table lookups by
 // XOR/shift, bit1 skips the in-lane fold, bit2 drops the per-round wave-priority rotation;
