@@ -1403,6 +1403,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
+static_assert(WTP_BR_HOLD == 16, "product build: held results stored every 16 flushes");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");
@@ -2054,6 +2055,9 @@ int launch_fixed_braid_rows(DevState &s, const uint8_t *base, uint64_t stride, u
                             hipStream_t st, unsigned grid, unsigned threads, int rows);
 #ifndef WTP_BR_HOLD_ROUNDS
 #define WTP_BR_HOLD_ROUNDS 64  // rounds per wave from which the CRC holds its results (CrcHoldBEpi)
+#endif
+#ifndef WTP_AB_BUILD
+static_assert(WTP_BR_HOLD_ROUNDS == 64, "product build: held results from 64 rounds per wave");
 #endif
 
 template <class BEpi>
