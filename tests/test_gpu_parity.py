@@ -107,6 +107,31 @@ def test_fixed_held_results_every_row_count(W, length, stride):
     assert bad.size == 0, f"{bad.size} mismatches, first at packets {idx[bad[:5]]}"
 
 
+def test_fixed_held_results_fuzz(W):
+    """Seeded fuzz of long fixed batches (the held-results epilogue): random 16-B multiple
+    lengths 16-1536, strides up to 1 KiB above them, n from 508 K to 1.2 M (odd counts,
+    partial last rounds and dumps), a buffer offset that keeps 16-B alignment; sampled and
+    tail packets against the oracle."""
+    rng = np.random.default_rng(20261017)
+    for case in range(6):
+        length = 16 * int(rng.integers(1, 97))
+        stride = length + 16 * int(rng.integers(0, 65))
+        n = int(rng.integers(508_000, 1_200_000)) | 1
+        lead = 16 * int(rng.integers(0, 8))
+        buf = torch.empty(lead + n * stride + 64, dtype=torch.uint8, device="cuda")
+        W.synth_fill(buf)
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        W.crc32_batch_fixed(buf[lead:], stride, length, n, out)
+        torch.cuda.synchronize()
+        idx = np.unique(np.concatenate([rng.integers(0, n, 200), np.arange(n - 130, n)]))
+        got = out[torch.from_numpy(idx).cuda()].cpu().numpy().view(np.uint32)
+        want = np.array([O.crc32(O.synth_fill_np(length, start_byte=lead + int(i) * stride)) for i in idx],
+                        dtype=np.uint32)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (case, length, stride, n, lead, idx[bad[:5]])
+        del buf, out
+
+
 def test_reserve_cus_keeps_results(W, golden):
     """wtp_reserve_cus shrinks the persistent grids; results stay bit-exact (golden
     4096 x 1456 digest, a long batch past the 64-rounds-per-wave grid rule, and a mixed
