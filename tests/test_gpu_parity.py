@@ -748,6 +748,46 @@ def test_verify_fast_path(W, n, stride, frac, with_crc):
     assert 0 < want_ok.sum() < n or frac == 1.0 or frac == 0.0
 
 
+def _long_ring(n, stride, rng):
+    """A long receive ring built with numpy (n in the hundreds of thousands): full WTP
+    datagrams with 16 + (stride - 16)-B lengths and, on a few percent, short receive
+    lengths, runts, oversize lengths, payload and header-checksum bit flips."""
+    L = stride - 16
+    body = O.synth_fill_np(n * L, start_byte=11)
+    crcs = O.batch_fixed(body, L, L, n, threads=8)
+    buf = np.zeros((n, stride), dtype=np.uint8)
+    buf[:, 16:] = body.reshape(n, L)
+    hdr = np.stack([np.full(n, 2, np.uint32), np.arange(n, dtype=np.uint32), np.full(n, L, np.uint32), crcs], axis=1)
+    buf[:, :16] = hdr.astype(">u4").view(np.uint8).reshape(n, 16)
+    rl = np.full(n, stride, dtype=np.uint32)
+    k = n // 100
+    idx = rng.choice(n, 5 * k, replace=False)
+    rl[idx[:k]] = 16 + rng.integers(0, L, k).astype(np.uint32)        # short: the fix-up phase
+    rl[idx[k:2 * k]] = rng.integers(0, 16, k).astype(np.uint32)       # runts
+    rl[idx[2 * k:3 * k]] = stride + rng.integers(1, 40, k).astype(np.uint32)  # oversize
+    for i in idx[3 * k:4 * k]:
+        buf[i, 16 + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    buf[idx[4 * k:], 12] ^= 0x10
+    return buf.reshape(-1), rl
+
+
+@pytest.mark.parametrize("stride", [1472, 1504])
+def test_verify_long_ring_with_fixups(W, stride):
+    """Rings long enough for the long-batch rules (>= 64 rounds per wave), with listed
+    datagrams spread over every workgroup: every ok and crc against the oracle (the fix-up
+    phase rewrites entries the braided pass wrote first)."""
+    n = 600_003
+    rng = np.random.default_rng(stride)
+    buf, rl = _long_ring(n, stride, rng)
+    want_ok, want_crc = O.verify_datagrams(buf, stride, rl)
+    ok, crc = _verify_dev(W, buf, stride, rl, n, True)
+    assert np.array_equal(ok, want_ok), np.nonzero(ok != want_ok)[0][:10]
+    assert np.array_equal(crc, want_crc), np.nonzero(crc != want_crc)[0][:10]
+    ok2, _ = _verify_dev(W, buf, stride, rl, n, False)
+    assert np.array_equal(ok2, want_ok)
+    assert 0 < want_ok.sum() < n
+
+
 def _wtp_ring(n, stride, rng):
     """wReceiver's ring: 1504-B slots holding up to 1500 received bytes.  Mostly full
     WTP DATA datagrams (1472 B), some 1473-1500 B (non-WTP senders; the reference CRCs

@@ -43,10 +43,10 @@ st = torch.cuda.current_stream()
 sp = st.cuda_stream
 n = a.n
 P = 1456
-if a.what in ("build", "crc", "verify", "crcalt"):
-    # crcalt: two n-packet batches in one 2n buffer, the calls alternate between them (no
+if a.what in ("build", "crc", "verify", "crcalt", "verifyalt"):
+    # crcalt / verifyalt: two n-packet batches (rings), the calls alternate between them (no
     # launch re-reads what the previous one read: a streaming sender / receiver)
-    halves = 2 if a.what == "crcalt" else 1
+    halves = 2 if a.what in ("crcalt", "verifyalt") else 1
     pay = torch.empty(halves * n * P + 64, dtype=torch.uint8, device="cuda")
     L0.wtp_synth_fill(pay.data_ptr(), 0, halves * n * P, 0x5EED, sp)
     ncall = [0]
@@ -56,6 +56,9 @@ if a.what in ("build", "crc", "verify", "crcalt"):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     ref_wire = wire.clone()
+    if a.what == "verifyalt":
+        wire2 = torch.empty(n * 1472 + 64, dtype=torch.uint8, device="cuda")
+        L0.wtp_build_data_packets(pay.data_ptr() + n * P, n * P, 0, wire2.data_ptr(), 1472, wl.data_ptr(), sp)
 if a.what == "c5":
     lens = O.zipf_lengths(n, s=1.1)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
@@ -77,6 +80,10 @@ def call(L):
         L.wtp_crc32_batch_fixed(pay.data_ptr() + (ncall[0] % 2) * n * P, P, P, n, out.data_ptr(), sp)
     elif a.what == "verify":
         L.wtp_crc32_verify_batch(wire.data_ptr(), 1472, wl.data_ptr(), n, ok.data_ptr(), None, sp)
+    elif a.what == "verifyalt":
+        ncall[0] += 1
+        L.wtp_crc32_verify_batch((wire2 if ncall[0] % 2 else wire).data_ptr(), 1472, wl.data_ptr(), n, ok.data_ptr(),
+                                 None, sp)
     elif a.what == "c5":
         L.wtp_crc32_batch_var(d.data_ptr(), total, do.data_ptr(), dl.data_ptr(), n, out.data_ptr(), sp)
 
