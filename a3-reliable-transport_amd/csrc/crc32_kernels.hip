@@ -354,12 +354,6 @@ struct VerifyBEpi {
     }
 };
 
-// The same epilogue for long rings (WTP_BR_VHOLD): k_fixed_braid holds ok and crc in LDS
-// and stores them in bursts before the fix-up phase (see kDumpV there).
-struct VerifyHoldBEpi : VerifyBEpi {
-    static constexpr bool kHold = true;
-};
-
 // Fused DATA packet builder (Packet.cpp:9-14,40-47,
 // Sender.cpp:187-197): payload p (stride len) -> wire[p*wstride ..) = big-endian
 // PacketHeader{DATA, seq0 + p, len, crc} || payload.  kCopy: every 16-B chunk the
@@ -601,46 +595,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
             dgroups = 0;
         }
     };
-    // Verify (VerifyHoldBEpi): 12 flushes of ok bytes (384 B) and crc words (1536 B) in the
-    // same 2 KiB buffer, stored in bursts; the last burst completes before the fix-up phase
-    // rewrites the datagrams it lists.
-    constexpr bool kDumpV = BEpi::kHold && BEpi::kFixup;
-    constexpr uint32_t kHoldV = 12, kOkOff = kHoldV * 8 * 16;
-    const bool holdv = kDumpV && nwave <= 8;
-    auto dumpv = [&]() {
-        if constexpr (kDumpV) {
-            __builtin_amdgcn_wave_barrier();
-            const uint64_t pb0 = 4 * dfirst, left = n > pb0 ? n - pb0 : 0;
-            const uint32_t rec4 = left >= (1ull << 29) ? 0x80000000u : uint32_t(4 * left);
-            const uint32_t rec1 = left >= (1ull << 29) ? 0x80000000u : uint32_t(left);
-            const __amdgpu_buffer_rsrc_t crs = make_rsrc(epi.crc ? epi.crc + pb0 : nullptr, epi.crc ? rec4 : 0u);
-            const __amdgpu_buffer_rsrc_t okr = make_rsrc(epi.ok + pb0, rec1);
-#pragma unroll
-            for (uint32_t t = 0; t < (kHoldV * 8 + 63) / 64; ++t) {
-                const uint32_t si = lane + 64u * t;  // segment: flush si >> 3, row si & 7
-                const bool inb = si < kHoldV * 8;
-                const u32x4 v = *(const lu32x4 *)(rbuf + (inb ? si : 0u) * 16u);
-                const uint32_t okw = *(const __attribute__((address_space(3))) uint32_t *)(rbuf + kOkOff + (inb ? si : 0u) * 4u);
-                const uint64_t rr = dfirst + (8u * uint64_t(si >> 3) + (si & 7u)) * rstep;
-                const uint64_t pb = 4 * rr;
-                const uint32_t o = uint32_t(pb - pb0);
-                const bool live = inb && (si >> 3) < dgroups && rr < rounds;
-                if (__builtin_amdgcn_ballot_w64(live && pb + 4 > n) == 0) {
-                    __builtin_amdgcn_raw_buffer_store_b128(v, crs, live ? int(4 * o) : int(0x80000000u), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(okw, okr, live ? int(o) : int(0x80000000u), 0, 0);
-                } else {
-#pragma unroll
-                    for (uint32_t e = 0; e < 4; ++e) {
-                        const bool on1 = live && pb + e < n;
-                        __builtin_amdgcn_raw_buffer_store_b32(v[e], crs, on1 ? int(4 * (o + e)) : int(0x80000000u), 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(okw >> (8 * e)), okr, on1 ? int(o + e) : int(0x80000000u), 0, 0);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            dgroups = 0;
-        }
-    };
     auto group_packet = [&](uint64_t g0) { return (g0 + uint64_t(lane >> 3) * rstep) * 4 + ((lane >> 1) & 3u); };
 
     auto flush = [&](uint64_t next_g0, bool more) {
@@ -673,22 +627,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
         // every x^-k above): once per packet instead of four times per lane per round
         if (!(DIAG & 1)) acc = stag_apply3<0>(lds, K.kA, K.sel, acc);
         const bool on = h == 0 && (lane >> 3) < k && rr < rounds && p < n;
-        if constexpr (kDumpV) {
-            if (holdv) {
-                if (dgroups == 0) dfirst = rfirst;
-                if (h == 0) {
-                    const uint32_t c = acc ^ epi.cinit;
-                    const bool mine = pre.r == epi.full;
-                    const uint32_t seg = dgroups * 8u + (lane >> 3), qq = (lane >> 1) & 3u;
-                    *(__attribute__((address_space(3))) uint32_t *)(rbuf + seg * 16u + qq * 4u) = mine ? c : 0u;
-                    *(__attribute__((address_space(3))) uint8_t *)(rbuf + kOkOff + seg * 4u + qq) =
-                        uint8_t(mine && bswap32(pre.h) == c ? 1 : 0);
-                }
-                if (++dgroups == kHoldV) dumpv();
-            } else {
-                epi.put(p, acc, on, pre);
-            }
-        } else if constexpr (kDump) {
+        if constexpr (kDump) {
             if (hold) {  // the buffer sits in the transposition slots of waves 8..15
                 if (dgroups == 0) dfirst = rfirst;
                 // flush dgroups, row lane >> 3, packet (lane >> 1) & 3: segment 8 dgroups + row
@@ -823,10 +762,6 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
     if (k) flush(0, false);
     if constexpr (kDump) {
         if (dgroups) dump();
-    }
-    if constexpr (kDumpV) {
-        if (dgroups) dumpv();
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the bursts land before the fix-up rewrites
     }
     PC_PROBE(5, __builtin_amdgcn_s_memrealtime());
     if constexpr (BEpi::kFixup) verify_fixup(lds, epi, gtab, nfix, rstep, wave, lane);
@@ -2121,9 +2056,6 @@ int launch_fixed_braid_rows(DevState &s, const uint8_t *base, uint64_t stride, u
 #ifndef WTP_BR_HOLD_ROUNDS
 #define WTP_BR_HOLD_ROUNDS 64  // rounds per wave from which the CRC holds its results (CrcHoldBEpi)
 #endif
-#ifndef WTP_BR_VHOLD
-#define WTP_BR_VHOLD 0  // long verify rings hold ok / crc in LDS (VerifyHoldBEpi; A/B builds: 1)
-#endif
 #ifndef WTP_AB_BUILD
 static_assert(WTP_BR_HOLD_ROUNDS == 64, "product build: held results from 64 rounds per wave");
 #endif
@@ -2152,13 +2084,6 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
         if (rounds >= uint64_t(WTP_BR_HOLD_ROUNDS) * grid * (threads / 64)) {
             dev::CrcHoldBEpi h;
             static_cast<dev::CrcBEpi &>(h) = epi;
-            return launch_fixed_braid_rows(s, base, stride, len, n, h, st, grid, threads, rows);
-        }
-    }
-    if constexpr (std::is_same_v<BEpi, dev::VerifyBEpi>) {
-        if (WTP_BR_VHOLD && rounds >= uint64_t(WTP_BR_HOLD_ROUNDS) * grid * (threads / 64)) {
-            dev::VerifyHoldBEpi h;
-            static_cast<dev::VerifyBEpi &>(h) = epi;
             return launch_fixed_braid_rows(s, base, stride, len, n, h, st, grid, threads, rows);
         }
     }
