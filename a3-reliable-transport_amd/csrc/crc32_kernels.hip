@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 #include <string>
 #include <vector>
@@ -193,22 +194,50 @@ struct StagSet {
 // load() issues the loads, store() writes LDS: a kernel issues the table loads before
 // its first data loads, since vmcnt completes in order and the table writes would
 // otherwise wait for the first round's data (the fill ended 4.4 us after entry).
+#ifndef WTP_FILL_X4
+#define WTP_FILL_X4 0  // 1: 16-B table loads, each feeding 4 stores (A/B builds; <= 512 threads)
+#endif
 template <int NS, int THREADS>
 struct StagFill {
     static_assert(THREADS <= 1024 && 2048 % THREADS == 0, "StagFill");
-    static constexpr int PER = NS * 2048 / THREADS;  // 16-B stores per thread (see fill_stag)
-    uint32_t v[PER];
+    // X4 form: load slot s of a set (512 per set) covers table t = (s >> 1) & 3, entries
+    // 4g .. 4g+3 (g = s >> 3), half h = s & 1 of their 8 copies: one 16-B global load, four
+    // 16-B LDS stores (each 8-lane group still writes 128 contiguous bytes of one row)
+    static constexpr bool kX4 = WTP_FILL_X4 && THREADS <= 512;
+    static constexpr int PER = kX4 ? NS * 512 / THREADS : NS * 2048 / THREADS;  // loads per thread
+    typename std::conditional<kX4, u32x4, uint32_t>::type v[PER];
     __device__ __forceinline__ void load(const StagSet (&sets)[NS]) {
+        if constexpr (kX4) {
 #pragma unroll
-        for (int k = 0; k < PER; ++k)
-            v[k] = sets[(k * THREADS) >> 11].g[stag_fill_word((uint32_t(k * THREADS) + threadIdx.x) & 2047u)];
+            for (int k = 0; k < PER; ++k) {
+                const uint32_t sidx = (uint32_t(k * THREADS) + threadIdx.x) & 511u;
+                v[k] = *reinterpret_cast<const u32x4 *>(sets[(k * THREADS) >> 9].g + ((sidx >> 1) & 3u) * 256u +
+                                                        4u * (sidx >> 3));
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+                v[k] = sets[(k * THREADS) >> 11].g[stag_fill_word((uint32_t(k * THREADS) + threadIdx.x) & 2047u)];
+        }
     }
     __device__ __forceinline__ void store(char *lds, const StagSet (&sets)[NS]) const {
+        if constexpr (kX4) {
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const uint32_t j = (uint32_t(k * THREADS) + threadIdx.x) & 2047u;
-            *reinterpret_cast<u32x4 *>(lds + sets[(k * THREADS) >> 11].off + stag_fill_off(j)) =
-                u32x4{v[k], v[k], v[k], v[k]};
+            for (int k = 0; k < PER; ++k) {
+                const uint32_t sidx = (uint32_t(k * THREADS) + threadIdx.x) & 511u;
+                const uint32_t base = sets[(k * THREADS) >> 9].off + (sidx >> 3) * 1024u + ((sidx >> 1) & 3u) * 32u +
+                                      (sidx & 1u) * 16u;
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i)
+                    *reinterpret_cast<u32x4 *>(lds + base + i * 256u) = u32x4{v[k][i], v[k][i], v[k][i], v[k][i]};
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const uint32_t j = (uint32_t(k * THREADS) + threadIdx.x) & 2047u;
+                *reinterpret_cast<u32x4 *>(lds + sets[(k * THREADS) >> 11].off + stag_fill_off(j)) =
+                    u32x4{v[k], v[k], v[k], v[k]};
+            }
         }
     }
 };
@@ -704,7 +733,7 @@ __global__ __launch_bounds__(BEpi::kBound) void k_fixed_braid(const uint8_t *__r
 #define WTP_BR_PROLOGUE_DIAG 0
 #endif
     if (batched && WTP_BR_PROLOGUE_DIAG == 0) fill.load(sets);
-    if (WTP_BR_PROLOGUE_DIAG == 1)
+    if constexpr (WTP_BR_PROLOGUE_DIAG == 1)
         for (int kk = 0; kk < fill.PER; ++kk) fill.v[kk] = threadIdx.x + kk;
     epi.pre(group_packet(r), pre);
     load_round(r, A);
