@@ -195,14 +195,17 @@ struct StagSet {
 // its first data loads, since vmcnt completes in order and the table writes would
 // otherwise wait for the first round's data (the fill ended 4.4 us after entry).
 #ifndef WTP_FILL_X4
-#define WTP_FILL_X4 0  // 1: 16-B table loads, each feeding 4 stores (A/B builds; <= 512 threads)
+#define WTP_FILL_X4 1  // 16-B table loads, each feeding 4 stores (<= 512 threads; 0: one dword per store, A/B builds)
 #endif
 template <int NS, int THREADS>
 struct StagFill {
     static_assert(THREADS <= 1024 && 2048 % THREADS == 0, "StagFill");
     // X4 form: load slot s of a set (512 per set) covers table t = (s >> 1) & 3, entries
     // 4g .. 4g+3 (g = s >> 3), half h = s & 1 of their 8 copies: one 16-B global load, four
-    // 16-B LDS stores (each 8-lane group still writes 128 contiguous bytes of one row)
+    // 16-B LDS stores (each 8-lane group still writes 128 contiguous bytes of one row).
+    // A quarter of the prologue's vector memory instructions: C2 (64 K packets) 15.46 ->
+    // 14.29 us from a graph, 16 K 7.03 -> 5.98, 1 M 216.5 -> 214.9 (interleaved,
+    // profiles/r04fx).
     static constexpr bool kX4 = WTP_FILL_X4 && THREADS <= 512;
     static constexpr int PER = kX4 ? NS * 512 / THREADS : NS * 2048 / THREADS;  // loads per thread
     typename std::conditional<kX4, u32x4, uint32_t>::type v[PER];
@@ -1432,7 +1435,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
-static_assert(WTP_BR_HOLD == 16, "product build: held results stored every 16 flushes");
+static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1, "product build: held results every 16 flushes, 16-B table fill");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");
