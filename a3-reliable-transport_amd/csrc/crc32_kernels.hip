@@ -194,6 +194,9 @@ struct StagSet {
 // load() issues the loads, store() writes LDS: a kernel issues the table loads before
 // its first data loads, since vmcnt completes in order and the table writes would
 // otherwise wait for the first round's data (the fill ended 4.4 us after entry).
+#ifndef WTP_FILL_X4_PC
+#define WTP_FILL_X4_PC 0  // the same for the piece kernel's 1024-thread fill (A/B builds)
+#endif
 #ifndef WTP_FILL_X4
 #define WTP_FILL_X4 1  // 16-B table loads, each feeding 4 stores (<= 512 threads; 0: one dword per store, A/B builds)
 #endif
@@ -206,7 +209,7 @@ struct StagFill {
     // A quarter of the prologue's vector memory instructions: C2 (64 K packets) 15.46 ->
     // 14.29 us from a graph, 16 K 7.03 -> 5.98, 1 M 216.5 -> 214.9 (interleaved,
     // profiles/r04fx).
-    static constexpr bool kX4 = WTP_FILL_X4 && THREADS <= 512;
+    static constexpr bool kX4 = WTP_FILL_X4 && (THREADS <= 512 || WTP_FILL_X4_PC);
     static constexpr int PER = kX4 ? NS * 512 / THREADS : NS * 2048 / THREADS;  // loads per thread
     typename std::conditional<kX4, u32x4, uint32_t>::type v[PER];
     __device__ __forceinline__ void load(const StagSet (&sets)[NS]) {
@@ -214,8 +217,16 @@ struct StagFill {
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
                 const uint32_t sidx = (uint32_t(k * THREADS) + threadIdx.x) & 511u;
-                v[k] = *reinterpret_cast<const u32x4 *>(sets[(k * THREADS) >> 9].g + ((sidx >> 1) & 3u) * 256u +
-                                                        4u * (sidx >> 3));
+                if constexpr (THREADS <= 512) {  // one set per k
+                    v[k] = *reinterpret_cast<const u32x4 *>(sets[(k * THREADS) >> 9].g + ((sidx >> 1) & 3u) * 256u +
+                                                            4u * (sidx >> 3));
+                } else {  // the set as an offset from set 0 (a select between pointers would be flat)
+                    const uint32_t si = (uint32_t(k * THREADS) + threadIdx.x) >> 9;
+                    ptrdiff_t gofs = 0;
+#pragma unroll
+                    for (int i = 1; i < NS; ++i) gofs = si == uint32_t(i) ? sets[i].g - sets[0].g : gofs;
+                    v[k] = *reinterpret_cast<const u32x4 *>(sets[0].g + gofs + ((sidx >> 1) & 3u) * 256u + 4u * (sidx >> 3));
+                }
             }
         } else {
 #pragma unroll
@@ -228,8 +239,16 @@ struct StagFill {
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
                 const uint32_t sidx = (uint32_t(k * THREADS) + threadIdx.x) & 511u;
-                const uint32_t base = sets[(k * THREADS) >> 9].off + (sidx >> 3) * 1024u + ((sidx >> 1) & 3u) * 32u +
-                                      (sidx & 1u) * 16u;
+                uint32_t soff;
+                if constexpr (THREADS <= 512) {
+                    soff = sets[(k * THREADS) >> 9].off;
+                } else {
+                    const uint32_t si = (uint32_t(k * THREADS) + threadIdx.x) >> 9;
+                    soff = sets[0].off;
+#pragma unroll
+                    for (int i = 1; i < NS; ++i) soff = si == uint32_t(i) ? sets[i].off : soff;
+                }
+                const uint32_t base = soff + (sidx >> 3) * 1024u + ((sidx >> 1) & 3u) * 32u + (sidx & 1u) * 16u;
 #pragma unroll
                 for (uint32_t i = 0; i < 4; ++i)
                     *reinterpret_cast<u32x4 *>(lds + base + i * 256u) = u32x4{v[k][i], v[k][i], v[k][i], v[k][i]};
@@ -1435,7 +1454,8 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
-static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1, "product build: held results every 16 flushes, 16-B table fill");
+static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 0,
+              "product build: held results every 16 flushes, 16-B table fill (braided kernels)");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");
