@@ -11,6 +11,7 @@
 #include <sys/time.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -132,9 +133,18 @@ class Checksums {
         for (size_t i = 0; i < n; ++i) b += rl[i] > kHeaderBytes ? std::min<size_t>(rl[i], stride) - kHeaderBytes : 0;
         return b;
     }
+    // WTP_VERIFY_CPU_MAX_BYTES: a plain decimal byte count (0 = every batch to the GPU).
+    // Anything else ("64K", "abc", out of range) is rejected: strtoull would read it as 0,
+    // which is a valid setting, so a typo would silently send every batch to the GPU.
     static size_t cpu_max_from_env() {
         const char *e = std::getenv("WTP_VERIFY_CPU_MAX_BYTES");
-        return e && *e ? size_t(std::strtoull(e, nullptr, 10)) : kCpuVerifyMaxBytes;
+        if (!e || !*e) return kCpuVerifyMaxBytes;
+        char *end = nullptr;
+        errno = 0;
+        const unsigned long long v = std::strtoull(e, &end, 10);
+        if (errno != 0 || end == e || *end != '\0' || *e == '-' || *e == '+' || *e == ' ')
+            throw std::invalid_argument(std::string("WTP_VERIFY_CPU_MAX_BYTES: not a decimal byte count: '") + e + "'");
+        return size_t(v);
     }
     bool gpu_;
     int gpus_;

@@ -339,6 +339,7 @@ struct CrcBEpi {  // out[p] = crc
     static constexpr int kBound = 1024;   // __launch_bounds__ (kbench A/B builds launch up to 1024)
     static constexpr int kLoadAux = 2;   // rows >= 1 stream (nt); row 0 is temporal (see k_fixed_braid)
     static constexpr bool kHold = false;  // CrcHoldBEpi: results held in LDS, stored in bursts
+    static constexpr const char *kName = "CrcBEpi";  // wtp_last_kernel()
     __device__ __forceinline__ uint32_t lead(uint64_t, uint32_t st, uint32_t len, uint32_t frame) const {
         return braid_lead(st, len, frame);
     }
@@ -355,6 +356,7 @@ struct CrcBEpi {  // out[p] = crc
 // LDS and stores them in bursts (see kDump there).
 struct CrcHoldBEpi : CrcBEpi {
     static constexpr bool kHold = true;
+    static constexpr const char *kName = "CrcHoldBEpi";
 };
 // Receiver verify over a datagram ring: the kernel runs on base = ring + 16 with the
 // ring's "full" payload length len (1456 for a WTP ring: 1472-B datagrams, whatever the
@@ -366,6 +368,7 @@ struct CrcHoldBEpi : CrcBEpi {
 // reference's semantics: one launch, no state outside the caller's buffers.
 struct VerifyBEpi {
     static constexpr bool kHold = false;  // see CrcBEpi
+    static constexpr const char *kName = "VerifyBEpi";
     static constexpr bool kCopy = false;
     static constexpr bool kFixup = true;  // see VerifyBEpi
     static constexpr int kThreads = 512;  // verify_fixup's LDS layout assumes 8 waves
@@ -435,6 +438,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
 #endif
 struct BuildBEpi {
     static constexpr bool kHold = false;  // see CrcBEpi
+    static constexpr const char *kName = "BuildBEpi";
     static constexpr bool kCopy = true;
     static constexpr bool kFixup = false;  // see VerifyBEpi
     // launched at 128 threads: the bound lets the copy rows keep their registers (at the
@@ -832,6 +836,7 @@ struct MetaRaw {
     uint32_t b, c, d;
 };
 struct CrcEpi {
+    static constexpr const char *kName = "CrcEpi";  // wtp_last_kernel()
     uint32_t *out;
     uint32_t n;
     __device__ __forceinline__ void put(uint64_t p, uint32_t crc, bool, uint32_t, bool on) const {
@@ -841,6 +846,7 @@ struct CrcEpi {
 // Receiver.cpp:203-206: (int)ntohl(hdr.checksum) == (int)crc32(payload).  aux carries the
 // header checksum (host order) from the provider.
 struct VerifyEpi {
+    static constexpr const char *kName = "VerifyEpi";
     uint8_t *ok;
     uint32_t *crc;  // may be null
     uint32_t n;
@@ -1465,6 +1471,7 @@ typedef __attribute__((address_space(3))) uint32_t lu32;
 
 // Datagram list[p] of the ring (lead 0: the ring is 16-B aligned); aux = ntohl(checksum).
 struct LdsIdxDgramProv {
+    static constexpr const char *kName = "LdsIdxDgramProv";  // wtp_last_kernel()
     static constexpr bool kVarLen = false;
     static constexpr bool kIndexed = true;
     static constexpr bool kGroupLoad = false;
@@ -1965,6 +1972,17 @@ __global__ void k_synth(uint8_t *__restrict__ out, uint64_t start, uint64_t nbyt
 namespace {
 
 thread_local std::string g_err;
+thread_local std::string g_kernel;  // wtp_last_kernel(): the calling thread's last launch
+
+void note_kernel(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void note_kernel(const char *fmt, ...) {
+    char buf[128];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_kernel = buf;
+}
 
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char *fmt, ...) {
@@ -2096,6 +2114,7 @@ static_assert(dev::VerifyBEpi::kThreads == 64 * dev::kVfWaves, "verify fix-up LD
 template <int ROWS, class BEpi>
 void launch_braid_rows(dim3 grid, unsigned threads, hipStream_t st, const uint8_t *b, uint64_t stride, uint32_t len,
                        uint64_t n, BEpi epi, const uint32_t *tabs) {
+    note_kernel("k_fixed_braid<%d, %d, %s>", ROWS, BEpi::kDiag, BEpi::kName);
     hipLaunchKernelGGL((dev::k_fixed_braid<ROWS, BEpi::kDiag, BEpi>), grid, dim3(threads), 0, st, b,
                        uint32_t(stride), len, n, epi, tabs);
 }
@@ -2132,8 +2151,11 @@ int launch_fixed_braid(DevState &s, const uint8_t *base, uint64_t stride, uint32
     if constexpr (std::is_same_v<BEpi, dev::CrcBEpi>) {
         // long batches hold their results in LDS (k_fixed_braid, kDump): short ones store
         // directly, the held form's code was 1.4-1.7% slower on 16 K-64 K packets even with
-        // nothing held (profiles/r04u)
-        if (rounds >= uint64_t(WTP_BR_HOLD_ROUNDS) * grid * (threads / 64)) {
+        // nothing held (profiles/r04u).  The held form's bursts are 16-B stores at
+        // out + 16 k: only a 16-B aligned `out` takes it (a torch slice out[1:] is only
+        // 4-B aligned; it keeps the direct dword stores).
+        if (rounds >= uint64_t(WTP_BR_HOLD_ROUNDS) * grid * (threads / 64) &&
+            (reinterpret_cast<uintptr_t>(epi.out) & 15u) == 0) {
             dev::CrcHoldBEpi h;
             static_cast<dev::CrcBEpi &>(h) = epi;
             return launch_fixed_braid_rows(s, base, stride, len, n, h, st, grid, threads, rows);
@@ -2171,6 +2193,7 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
     uint64_t grid = (waves_want + dev::kPcThreads / 64 - 1) / (dev::kPcThreads / 64);
     if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
     if (grid == 0) grid = 1;
+    note_kernel("k_pieces<%s, %s>", Prov::kName, Epi::kName);
     hipLaunchKernelGGL((dev::k_pieces<Prov, Epi>), dim3(unsigned(grid)), dim3(dev::kPcThreads), 0, st, b16, uint32_t(span),
                        prov, n, epi, s.tabs, s.status);
     return launch_check("k_pieces");
@@ -2184,6 +2207,7 @@ int launch_stream(DevState &s, const uint8_t *base, uint64_t nbytes, const uint6
     uint64_t grid = (n + dev::kStWaves * 64 - 1) / (dev::kStWaves * 64);  // >= 64 payloads per wave
     if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
     if (grid == 0) grid = 1;
+    note_kernel("k_stream");
     hipLaunchKernelGGL((dev::k_stream<0>), dim3(unsigned(grid)), dim3(dev::kStThreads), 0, st, base - lead,
                        lead + nbytes, offs, lens, lead, n, out, s.tabs, s.status);
     return launch_check("k_stream");
@@ -2199,6 +2223,7 @@ namespace dev {
 // raw words into (offset in the view, length, valid, aux, output slot) when the round
 // uses them.  count(n) is the number of packets (device-side for the fix-up pass).
 struct FixedProvL {
+    static constexpr const char *kName = "FixedProvL";  // wtp_last_kernel()
     static constexpr bool kVarLen = false;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = false;
@@ -2213,6 +2238,7 @@ struct FixedProvL {
     }
 };
 struct ArrayProvL {
+    static constexpr const char *kName = "ArrayProvL";  // wtp_last_kernel()
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = true;  // load_group: 32-bit buffer offsets, no clamp
@@ -2247,6 +2273,7 @@ struct ArrayProvL {
 // the last datagram, reads there return 0 and are never selected) and are
 // funnel-shifted at decode.
 struct DgramProvL {
+    static constexpr const char *kName = "DgramProvL";  // wtp_last_kernel()
     static constexpr bool kVarLen = true;  // wave ranges balanced by pieces
     static constexpr bool kIndexed = false;
     static constexpr bool kGroupLoad = false;
@@ -2286,6 +2313,7 @@ extern "C" {
 const char *wtp_version(void) { return "wtp-crc32-mi355x 0.1 (gfx950)"; }
 
 const char *wtp_last_error(void) { return g_err.c_str(); }
+const char *wtp_last_kernel(void) { return g_kernel.c_str(); }
 
 int wtp_set_error_(int code, const char *msg) {
     g_err = msg ? msg : "";

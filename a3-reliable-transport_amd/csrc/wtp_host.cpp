@@ -91,9 +91,14 @@ int pipe_get(Pipe *&out) {
                 H_HIP(hipMalloc(reinterpret_cast<void **>(&p.dev_ok[b]), p.max_pk));
             }
             // the library's own pinned result buffers never move: look their device views
-            // up once, not per zero-copy call
-            H_HIP(hipHostGetDevicePointer(&p.view_ok0, p.pin_ok[0], 0));
-            H_HIP(hipHostGetDevicePointer(&p.view_out0, p.pin_out[0], 0));
+            // up once, not per zero-copy call.  Optional: without them only the
+            // zero-copy verify fast path is skipped, so a failed lookup leaves both null and
+            // clears the HIP error instead of failing the pipeline
+            if (hipHostGetDevicePointer(&p.view_ok0, p.pin_ok[0], 0) != hipSuccess ||
+                hipHostGetDevicePointer(&p.view_out0, p.pin_out[0], 0) != hipSuccess) {
+                p.view_ok0 = p.view_out0 = nullptr;
+                (void)hipGetLastError();
+            }
             return WTP_OK;
         };
         p.rc = mk();
@@ -384,7 +389,8 @@ int wtp_crc32_host_verify(const void *h_dgrams, size_t stride, const uint32_t *h
     if (rc) return rc;
     std::lock_guard<std::mutex> g(P->mu);
     const void *dr = dev_view(h_dgrams), *dl = dev_view(h_recv_len);
-    if (dr && dl && n <= P->max_pk && n * stride <= kZeroCopyBytes && zero_copy_enabled()) {
+    if (dr && dl && P->view_ok0 && P->view_out0 && n <= P->max_pk && n * stride <= kZeroCopyBytes &&
+        zero_copy_enabled()) {
         rc = host_verify_zero_copy(P, dr, stride, dl, n, P->view_ok0, P->view_out0, h_ok, h_crc_out);
     } else {
         // a pinned ring (wReceiver's recvmmsg ring) is copied to the device directly

@@ -36,6 +36,7 @@ def _load() -> C.CDLL:
     sig = {
         "wtp_version": (C.c_char_p, []),
         "wtp_last_error": (C.c_char_p, []),
+        "wtp_last_kernel": (C.c_char_p, []),
         "wtp_device_count": (i32, []),
         "wtp_init": (i32, [i32]),
         "wtp_device_status": (i32, [i32, C.POINTER(u32), i32]),
@@ -63,7 +64,7 @@ def _load() -> C.CDLL:
 
 
 LIB = _load()
-EXPORTED = ("wtp_version", "wtp_last_error", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_reserve_cus", "wtp_crc32",
+EXPORTED = ("wtp_version", "wtp_last_error", "wtp_last_kernel", "wtp_device_count", "wtp_init", "wtp_device_status", "wtp_reserve_cus", "wtp_crc32",
             "wtp_crc32_batch_fixed", "wtp_crc32_batch_var", "wtp_crc32_batch_packed", "wtp_crc32_verify_batch", "wtp_build_data_packets",
             "wtp_crc32_host_batch_fixed", "wtp_crc32_host_chunked", "wtp_crc32_host_chunked_multi", "wtp_crc32_host_verify",
             "wtp_host_build_data_packets", "wtp_host_alloc", "wtp_host_free", "wtp_synth_fill")

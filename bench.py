@@ -25,7 +25,7 @@ N = 1 adds two legs after the timed region (--no-extras skips them): alt_buffer 
 kernel alternating between two 1 M buffers, as a streaming sender would) and
 c4_shard_1gpu (rank 0's 2 M-packet C4 shard through the N > 1 pipelined step with a
 one-rank RCCL gather: the equal-work reference for the N > 1 lines).  N > 1 lines add
-per_rank_kernel_ms and step_ms.
+per-rank kernel and gather times, step_ms and overlap (rank_fields).
 Warmup: see settle() — untimed launches until the clock transient has passed.
 """
 from __future__ import annotations
@@ -203,8 +203,8 @@ def pmc_traffic(n_packets: int, lib_path: str, path: str | None = None):
     want = (d.get("kernel_code") or {}).get("sha256")
     try:
         have = codeobj.kernel_code_sha256(lib_path, codeobj.HEADLINE_KERNEL)["sha256"]
-    except (OSError, ValueError) as e:
-        return None, {"status": f"cannot hash the shipped kernel ({e})"}
+    except Exception as e:  # noqa: BLE001 — diagnostics only: any ELF-parse failure is reported, never fatal
+        return None, {"status": f"cannot hash the shipped kernel ({e.__class__.__name__}: {e})"}
     if want != have:
         return None, {"status": "stale: the shipped k_fixed_braid<6> code differs from the one the PMC pass measured",
                       "record_sha256": (want or "")[:16], "shipped_sha256": have[:16]}
@@ -393,6 +393,39 @@ class Pipe:
         self.pos = 0     # result slots used (a flush skips to the next group)
         self.last_m, self.last_g = 0, 0  # slots and group of the last gather
         self.last_pos = 0
+        self.timed = False  # time_steps sets it: the gathers issued meanwhile are timed
+        self.gather_rec = []
+        self._obs = None    # side stream that waits for each timed gather (event mode)
+
+    def _time_gather(self, work):
+        """Time one gather: from its inputs being ready (an event on the CRC stream, queued
+        right before the collective, i.e. after the step's CRC launch) to its completion on
+        the collective's stream (a side stream waits for the work, then records the end).
+        Without HIP streams (gloo CPU tests) the same span is taken on the host clock, from
+        the issue to the work's future completing."""
+        if hasattr(self.stream, "cuda_stream"):
+            import torch
+            if self._obs is None:
+                self._obs = torch.cuda.Stream()
+            end = TimingEvent()
+            with torch.cuda.stream(self._obs):
+                work.wait()
+                end.record(self._obs)
+            self.gather_rec[-1]["end"] = end
+        else:
+            rec = self.gather_rec[-1]
+            rec["t0"] = time.perf_counter()
+            work.get_future().then(lambda f, rec=rec: rec.__setitem__("t1", time.perf_counter()))
+
+    def gather_ms(self) -> list:
+        """Durations (ms) of the gathers issued while `timed` (call after drain())."""
+        out = []
+        for r in self.gather_rec:
+            if "end" in r:
+                out.append(r["start"].elapsed_time(r["end"]))
+            elif "t1" in r:
+                out.append((r["t1"] - r["t0"]) * 1e3)
+        return out
 
     def _group(self, pos):
         return (pos // self.K) % len(self.groups)
@@ -418,7 +451,15 @@ class Pipe:
         if self.gathered is not None:
             half = self.world * self.K * self.n
             out = self.gathered[g * half:g * half + self.world * m * self.n]
+        if self.timed:
+            rec = {"steps": m}
+            if hasattr(self.stream, "cuda_stream"):
+                rec["start"] = TimingEvent()
+                rec["start"].record(self.stream)
+            self.gather_rec.append(rec)
         self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
+        if self.timed and self.works[g] is not None:
+            self._time_gather(self.works[g])
         self.last_m, self.last_g = m, g
 
     def finish(self):
@@ -470,6 +511,7 @@ def time_steps(pipe: Pipe, steps: int, world: int):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    pipe.gather_rec, pipe.timed = [], True  # the gathers of these steps are timed (Pipe.gather_ms)
     t0 = time.perf_counter()
     for i in range(steps):
         pipe.wait_slot()  # (stream-side) before the start event: it times the kernel alone
@@ -482,7 +524,42 @@ def time_steps(pipe: Pipe, steps: int, world: int):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    pipe.timed = False
     return [s.elapsed_time(e) for s, e in zip(starts, ends)], el
+
+
+def rank_fields(kern_ms: list, gather_ms: list, el: float, steps: int, world: int, dev) -> tuple[float, dict]:
+    """The N > 1 line's per-rank fields (collectives: every rank must call this).  el =
+    this rank's wall seconds; returns (max over ranks of el, fields):
+      per_rank_kernel_ms, kernel_ms_max_over_ranks — mean CRC launch time per rank;
+      per_rank_gather_ms, gather_ms_max_over_ranks — mean time per gather collective,
+        from its inputs being ready to its completion on the collective's stream
+        (Pipe._time_gather); gathers_per_rank = collectives in the timed region;
+      step_ms — wall time per step (max over ranks);
+      overlap — step_ms - kernel_ms_max_over_ranks: the step time the kernels do not
+        explain.  About 0 when the gather hides behind the next CRC launches; about
+        gather_ms / gather_every when it serialises with them."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    km = sum(kern_ms) / len(kern_ms)
+    gm = sum(gather_ms) / len(gather_ms) if gather_ms else 0.0
+    mine = torch.tensor([km, gm, float(len(gather_ms))], dtype=torch.float64, device=dev)
+    allr = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    rows = [[float(v) for v in x.tolist()] for x in allr]
+    per_k = [round(r[0], 5) for r in rows]
+    per_g = [round(r[1], 5) for r in rows]
+    step_ms = round(el / steps * 1e3, 4)
+    return el, {"per_rank_kernel_ms": per_k, "kernel_ms_max_over_ranks": max(per_k),
+                "per_rank_gather_ms": per_g, "gather_ms_max_over_ranks": max(per_g),
+                "gathers_per_rank": [int(r[2]) for r in rows],
+                "step_ms": step_ms, "overlap": round(step_ms - max(per_k), 5),
+                "overlap_rule": "step_ms - kernel_ms_max_over_ranks: ~0 = gather hidden behind the CRC launches, "
+                                "~gather_ms / gather_every = serialised"}
 
 
 def kstats(kern: list, nbytes: int) -> dict:
@@ -521,6 +598,7 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
         pipe.drain()
         torch.cuda.synchronize()
         kern, el = time_steps(pipe, steps, 1)
+        gms = pipe.gather_ms()
         import numpy as np
         par = parity_digest(pipe.gathered_vector().cpu().numpy().view(np.uint32))
     finally:
@@ -535,6 +613,9 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
            "step_ms": round(el / steps * 1e3, 4), "value_GiBs": round(nbytes * steps / el / 2**30, 2),
            "parity_match": par["match"], "sha256": par["sha256"]}
     out.update(kstats(kern, nbytes))
+    out["gather_ms"] = round(sum(gms) / len(gms), 5) if gms else None
+    out["gathers"] = len(gms)
+    out["overlap"] = round(out["step_ms"] - out["kernel_ms_mean"], 5)
     del buf
     return out
 
@@ -635,18 +716,13 @@ def main():
     torch.cuda.synchronize()
 
     kern, el = time_steps(pipe, args.steps, world)
+    kernel_name = W.LIB.wtp_last_kernel().decode()  # the instantiation the timed launches used
     kern_ms = sorted(kern)
     kmean = sum(kern_ms) / len(kern_ms)
 
     per_rank = None
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        km = torch.tensor([kmean], dtype=torch.float64, device=dev)
-        allk = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
-        dist.all_gather(allk, km)
-        per_rank = [round(float(x.item()), 5) for x in allk]
+        el, per_rank = rank_fields(kern, pipe.gather_ms(), el, args.steps, world, dev)
 
     # parity of the WHOLE result vector (rank 0: the gathered vector when N > 1)
     parity = None
@@ -689,7 +765,7 @@ def main():
                    "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,
-                     "kernel": "k_fixed_braid<6, 0, CrcHoldBEpi>", "kernel_ms_mean": round(kmean, 5),
+                     "kernel": kernel_name, "kernel_ms_mean": round(kmean, 5),
                      "kernel_ms_median": round(kern_ms[len(kern_ms) // 2], 5),
                      "kernel_ms_p10": round(kern_ms[len(kern_ms) // 10], 5),
                      "kernel_ms_p90": round(kern_ms[(9 * len(kern_ms)) // 10], 5),
@@ -705,9 +781,7 @@ def main():
         "parity": parity,
     }
     if per_rank is not None:
-        line["per_rank_kernel_ms"] = per_rank
-        line["kernel_ms_max_over_ranks"] = max(per_rank)
-        line["step_ms"] = round(el / args.steps * 1e3, 4)
+        line.update(per_rank)
     extras = rank == 0 and world == 1 and not args.gather_n1 and n == 1 << 20 and not args.no_extras
     if extras:  # after the timed region and the probe: neither leg touches the headline numbers
         run_extra_legs(line, parity, W, shard, buf, nbytes, n, dev, local, stream, args)

@@ -62,6 +62,11 @@ const char *wtp_version(void);
 /* Message for the calling thread's last failure ("" if none). */
 const char *wtp_last_error(void);
 
+/* Kernel instantiation the calling thread's last launch used, e.g.
+   "k_fixed_braid<6, 0, CrcHoldBEpi>" ("" if none).  Diagnostics: bench.py names the
+   kernel its roofline measures with it. */
+const char *wtp_last_kernel(void);
+
 /* Number of visible HIP devices (0 when none). Does not create a context. */
 int wtp_device_count(void);
 

@@ -172,6 +172,9 @@ def test_n1_extra_legs_fields_on_cpu(monkeypatch, every):
     assert c4["sha256"] == hashlib.sha256(want.astype("<u4").tobytes()).hexdigest()[:16]
     assert c4["parity_match"] is None  # no reference digest at this size; the real leg has one
     assert {"kernel_ms_mean", "GBs", "frac", "step_ms", "value_GiBs"} <= set(c4)
+    # the timed gathers (full groups + the flushed partial one) and the step time beyond the kernel
+    assert c4["gathers"] == -(-4 // every) and c4["gather_ms"] > 0
+    assert abs(c4["overlap"] - (c4["step_ms"] - c4["kernel_ms_mean"])) < 1e-4
 
 
 def test_default_c4_leg_is_the_two_million_packet_shard():
@@ -182,23 +185,42 @@ def test_default_c4_leg_is_the_two_million_packet_shard():
     assert sig.parameters["n"].default == 2097152 == bench.C4_PACKETS // 8
 
 
-def test_traffic_null_unless_kernel_code_matches(tmp_path):
-    """roofline.traffic is the committed PMC pass's number only while the shipped
-    k_fixed_braid<6> has the code that pass measured: one flipped byte of the recorded
-    hash gives traffic null."""
+def test_pmc_record_matches_shipped_kernel():
+    """profiles/pmc_traffic.json (the PMC pass behind roofline.traffic) was measured on the
+    shipped k_fixed_braid<6>'s machine code.  This is the only test that fails on a stale
+    record: refresh it with tools/gpu_round.sh (its `pmcnew` step runs first whenever
+    tools/codeobj.py's hash differs) after a kernel change."""
     import bench
     sys.path.insert(0, os.path.join(ROOT, "a3-reliable-transport_amd"))
     import wtp_crc32 as W
     rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     v, info = bench.pmc_traffic(1 << 20, W.LIB_PATH)
     assert v == rec["hbm_bytes_per_launch"] and info["status"].startswith("measured"), info
-    h = rec["kernel_code"]["sha256"]
-    rec["kernel_code"]["sha256"] = ("0" if h[0] != "0" else "1") + h[1:]
+
+
+def test_traffic_null_unless_kernel_code_matches(tmp_path):
+    """roofline.traffic is a PMC record's number only while the shipped k_fixed_braid<6>
+    has the code that record names: a record stamped with the shipped hash is reported,
+    the same record with one flipped hex digit is null, another batch size is null.  (Built
+    on a copy stamped with the shipped hash, so it holds whether or not the committed
+    record is current: test_pmc_record_matches_shipped_kernel checks that.)"""
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "a3-reliable-transport_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import codeobj
+    import wtp_crc32 as W
+    rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    h = codeobj.kernel_code_sha256(W.LIB_PATH, codeobj.HEADLINE_KERNEL)["sha256"]
+    rec["kernel_code"]["sha256"] = h
     p = tmp_path / "pmc.json"
     p.write_text(json.dumps(rec))
     v, info = bench.pmc_traffic(1 << 20, W.LIB_PATH, str(p))
+    assert v == rec["hbm_bytes_per_launch"] and info["status"].startswith("measured"), info
+    rec["kernel_code"]["sha256"] = ("0" if h[0] != "0" else "1") + h[1:]
+    p.write_text(json.dumps(rec))
+    v, info = bench.pmc_traffic(1 << 20, W.LIB_PATH, str(p))
     assert v is None and info["status"].startswith("stale"), info
-    v, info = bench.pmc_traffic(2 << 20, W.LIB_PATH)
+    v, info = bench.pmc_traffic(2 << 20, W.LIB_PATH, str(p))
     assert v is None
 
 

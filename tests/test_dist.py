@@ -285,3 +285,73 @@ def test_bench_pipe_grouped_gather(world, every, steps):
     assert np.array_equal(got.view(np.uint32), want)
     # full groups of `every` results, then the partial group the drain flushes
     assert seen == [every] * (steps // every) + ([steps % every] if steps % every else [])
+
+
+class _WallEvent:
+    """Host-clock stand-in for bench.TimingEvent (no GPU here)."""
+
+    def record(self, stream):
+        import time
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
+def _rank_fields_worker(rank, world, port, every, steps, q):
+    """bench.py's N > 1 timed region (time_steps over its Pipe, gathers every `every`
+    steps) and its per-rank fields (rank_fields) over gloo, with a stand-in launch."""
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd")):
+        sys.path.insert(0, p)
+    import bench
+    import shard as S
+    bench.TimingEvent = _WallEvent
+    torch.cuda.synchronize = lambda *a: None
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 4099
+
+    class FakeW:
+        def crc32_batch_fixed(self, buf, stride, length, nn, out, stream=None):
+            out.copy_(torch.arange(nn, dtype=torch.int32) + rank)
+
+    gathered = torch.empty(2 * world * every * n, dtype=torch.int32) if rank == 0 else None
+    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every)
+    for _ in range(3):  # untimed warmup: its gathers are not counted
+        pipe.step()
+    pipe.drain()
+    kern, el = bench.time_steps(pipe, steps, world)
+    el_max, f = bench.rank_fields(kern, pipe.gather_ms(), el, steps, world, "cpu")
+    if rank == 0:
+        q.put((f, el_max, el))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,every,steps", [(8, 2, 5), (2, 1, 4)])
+def test_bench_rank_fields_gather_and_overlap(world, every, steps):
+    """The N > 1 line's overlap fields: per-rank gather time, gathers
+    per rank (the timed region's collectives only: full groups plus the flushed partial
+    one), overlap = step_ms - kernel_ms_max_over_ranks, maxima consistent with the lists."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_fields_worker, args=(r, world, port, every, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    f, el_max, el0 = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(f["per_rank_kernel_ms"]) == len(f["per_rank_gather_ms"]) == world
+    assert f["gathers_per_rank"] == [-(-steps // every)] * world
+    assert all(g > 0 for g in f["per_rank_gather_ms"]) and all(k > 0 for k in f["per_rank_kernel_ms"])
+    assert f["kernel_ms_max_over_ranks"] == max(f["per_rank_kernel_ms"])
+    assert f["gather_ms_max_over_ranks"] == max(f["per_rank_gather_ms"])
+    assert el_max >= el0 and f["step_ms"] == round(el_max / steps * 1e3, 4)
+    assert abs(f["overlap"] - (f["step_ms"] - f["kernel_ms_max_over_ranks"])) < 1e-4

@@ -66,6 +66,31 @@ def test_golden_batch_digest(W, golden):
     assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == g["sha256_le_u32"]
 
 
+def test_long_batch_into_unaligned_out(W):
+    """A long batch (1 M x 1456 B: >= 64 rounds per wave, the held-results rule) whose
+    result buffer is only 4-B aligned (out[1:] of a torch tensor): the held form stores
+    16-B bursts, so the launcher must take the direct-store kernel here.  The whole vector
+    equals the reference's 1 M digest, the guard word before it is untouched, and the
+    aligned call of the same batch takes the held kernel (wtp_last_kernel)."""
+    import json
+    n = 1 << 20
+    want = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_digests.json")))
+    want = want["sha256_by_packets"][str(n)]
+    buf = torch.empty(n * 1456, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    base = torch.full((n + 4,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    for shift, kern in ((1, "CrcBEpi"), (2, "CrcBEpi"), (3, "CrcBEpi"), (0, "CrcHoldBEpi"), (4, "CrcHoldBEpi")):
+        base.fill_(0x5A5A5A5A)
+        out = base[shift:shift + n]
+        assert (out.data_ptr() % 16 == 0) == (kern == "CrcHoldBEpi")
+        W.crc32_batch_fixed(buf, 1456, 1456, n, out)
+        assert W.LIB.wtp_last_kernel().decode() == f"k_fixed_braid<6, 0, {kern}>"
+        got = to_u32(out, n)
+        assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == want, shift
+        guard = base.cpu().numpy().view(np.uint32)
+        assert (guard[:shift] == 0x5A5A5A5A).all() and (guard[shift + n:] == 0x5A5A5A5A).all(), shift
+
+
 def test_fixed_held_results_past_2g_result_bytes(W):
     """Held results (CrcHoldBEpi, long batches) past 2^29 packets: 16-B payloads, n =
     2^29 + 1237 (8.6 GB of payloads, 2.1 GB of results), so result byte offsets pass 2^31

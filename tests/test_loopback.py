@@ -270,3 +270,14 @@ def test_batched_receive_bench_gpu(binaries, cpu_max):
     if cpu_max == "0":
         assert got["gpu_batches"] == got["batches"] and got["cpu_verify_max_bytes"] == 0, got
 
+
+
+@pytest.mark.parametrize("bad", ["64K", "abc", "-1", "99999999999999999999999"])
+def test_verify_cpu_max_bytes_rejects_unparsable(binaries, bad):
+    """WTP_VERIFY_CPU_MAX_BYTES must be a decimal byte count: strtoull would read '64K' or
+    'abc' as 0 (the documented 'every batch to the GPU' setting), so the endpoint refuses
+    such a value with a message instead of running a configuration nobody asked for."""
+    env = dict(os.environ, WTP_VERIFY_CPU_MAX_BYTES=bad)
+    r = subprocess.run([os.path.join(binaries, "wReceiver"), "--bench", "0", "-p", "1", "--crc", "cpu"],
+                       capture_output=True, text=True, timeout=30, env=env)
+    assert r.returncode != 0 and "WTP_VERIFY_CPU_MAX_BYTES" in r.stderr, (r.returncode, r.stderr)
