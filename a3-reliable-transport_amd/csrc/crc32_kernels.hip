@@ -835,10 +835,27 @@ struct MetaRaw {
     uint64_t a;
     uint32_t b, c, d;
 };
+// One sub-launch of a packed batch >= 2 GiB (launch_packed_ranges): packets [begin, end)
+// of the caller's arrays, read through a < 2 GiB view that starts `rebase` bytes into the
+// 16-B aligned buffer.  Written on the device by k_cut_ranges; `bad` is set by the piece
+// kernel when a packet lies outside the view (the offsets were not packed), and then a
+// gated k_stream launch recomputes the whole batch.
+struct RangeDesc {
+    uint64_t begin, end, rebase;
+    uint32_t nbytes, bad;
+};
+static_assert(sizeof(RangeDesc) == 32, "RangeDesc");
+// providers whose packet range and view are bound on the device (bind(), at kernel entry)
+template <class P>
+constexpr bool kDevRange = requires { P::kDevRange; };
 struct CrcEpi {
     static constexpr const char *kName = "CrcEpi";  // wtp_last_kernel()
     uint32_t *out;
     uint32_t n;
+    __device__ __forceinline__ void rebase(uint64_t first, uint32_t cnt) {  // a device-bound sub-range
+        out += first;
+        n = cnt;
+    }
     __device__ __forceinline__ void put(uint64_t p, uint32_t crc, bool, uint32_t, bool on) const {
         __builtin_amdgcn_raw_buffer_store_b32(crc, make_rsrc(out, 4 * n), on ? int(4 * p) : int(0x80000000u), 0, 0);
     }
@@ -1086,8 +1103,45 @@ struct SpanDma {
                              : "memory");
         }
     }
+    // The same, leaving out the chunks that start at or past view byte `lim` (their lanes
+    // get an out-of-range offset: no request).  The tail clamp (WTP_PC_TAILCLAMP) below.
+    __device__ __forceinline__ void issue_below(__amdgpu_buffer_rsrc_t rs, int32_t b16, uint32_t lane, int32_t lim) const {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t i = 0; i < kPcDmaRegs; ++i) {
+            const int32_t c0 = b16 + int32_t(coff[i]);
+            const uint32_t voff = c0 < lim ? uint32_t(c0) : 0x80000000u;
+            const uint32_t m0v = slot + 1024u * i;
+            uint32_t keep;
+            if (i + 1 < kPcDmaRegs || lane < kPcSlotPos - 64u * (kPcDmaRegs - 1))
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep)
+                             : "v"(voff), "s"(rs), "s"(m0v)
+                             : "memory");
+        }
+    }
     __device__ __forceinline__ static void wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t u = uint32_t(__shfl_xor(int(v), o));
+        v = u > v ? u : v;
+    }
+    return uint32_t(__builtin_amdgcn_readfirstlane(int(v)));
+}
+
+// Tail clamp of the span prefetch: a wave's last rounds used to prefetch a full 4352-B
+// span past the end of its last packet, i.e. into the first bytes of the next wave's
+// range, which that wave had read ~40 us earlier (its first round), so they came from
+// memory twice: ~3.4 KB per wave boundary, 14.1 MB of C5's 26 MB excess read
+// (tools/c5_span_model.py, profiles/r05).  When the round's view holds every packet the
+// wave has left, the prefetch stops at the end of the last of them.
+#ifndef WTP_PC_TAILCLAMP
+#define WTP_PC_TAILCLAMP 1
+#endif
 
 // The wave's packets form one stream of 64-B pieces (each packet cut into pieces counted
 // back from its end, the head piece possibly shorter).  A round takes the next pieces,
@@ -1158,6 +1212,9 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         prov.decode(raw, off, len, valid, aux, oslot);
         const uint32_t inview = hi - p0 > 64u ? 64u : uint32_t(hi - p0);  // wave-uniform (SALU)
         const bool have = lane < inview;
+        if constexpr (kDevRange<Prov>) {
+            if (have && !valid) prov.flag_outside();  // not packed: the gated k_stream redoes the batch
+        }
         if (have && len > kMaxVarLen) {
             atomicOr(status, 1u);
             len = 0;
@@ -1254,7 +1311,16 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         meta(p0n);  // first: the next round waits for these, not for the span
         spec = p0n < hi ? ((last_we - kPieceS) & ~15) : kNoSpan;
 #if WTP_PC_DMA
-        if (spec != kNoSpan) dma.issue(rs, spec, lane);  // wave-uniform branch
+        // (not in the verify fix-up's indexed pass: scattered datagrams, and its kernel has
+        // no SGPRs to spare for it)
+        if (WTP_PC_TAILCLAMP && !Prov::kIndexed && spec != kNoSpan && hi - p0 <= 64u) {  // wave-uniform: the wave's last packets are all in view
+            // end of the bytes any packet still to do can need (lanes from the round's last
+            // packet on: a superset of p0n .. hi-1)
+            const uint32_t pend = have && lane >= last_pk ? uint32_t(off) + len : 0u;
+            dma.issue_below(rs, spec, lane, int32_t(wave_max_u32(pend)));
+        } else if (spec != kNoSpan) {
+            dma.issue(rs, spec, lane);  // wave-uniform branch
+        }
 #else
         load_span(rs, spec, lane, x);
 #endif
@@ -1384,11 +1450,19 @@ struct PcTables {
 };
 
 template <class Prov, class Epi>
-__global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base, uint32_t nbytes, Prov prov,
-                                                 uint64_t n, Epi epi, const uint32_t *__restrict__ gtab,
-                                                 uint32_t *__restrict__ status) {
+__global__ __launch_bounds__(kPcThreads) void k_pieces(const uint8_t *__restrict__ base_in, uint32_t nbytes_in,
+                                                 Prov prov_in, uint64_t n_in, Epi epi_in,
+                                                 const uint32_t *__restrict__ gtab, uint32_t *__restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kPcLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
+    Prov prov = prov_in;
+    Epi epi = epi_in;
+    const uint8_t *base = base_in;
+    uint32_t nbytes = nbytes_in;
+    uint64_t n = n_in;
+    if constexpr (kDevRange<Prov>) {
+        if (!prov.bind(base, nbytes, n, epi)) return;  // this sub-launch's range is empty
+    }
     const uint32_t nw = blockDim.x >> 6;
     const uint64_t tw = uint64_t(gridDim.x) * nw, w0 = uint64_t(blockIdx.x) * nw;
     const uint64_t g0 = n * w0 / tw, g1 = n * (w0 + nw) / tw;  // this workgroup's packets
@@ -1457,7 +1531,8 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 // pprobe) define WTP_AB_BUILD to build variants.  A misconfigured product build is a
 // compile error, not a library that runs wrong.
 #ifndef WTP_AB_BUILD
-static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1,
+static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1 &&
+                  WTP_PC_TAILCLAMP == 1,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
 static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 0,
@@ -1635,9 +1710,17 @@ __global__ __launch_bounds__(kStThreads) void k_stream(const uint8_t *__restrict
                                                      const uint64_t *__restrict__ offs,
                                                      const uint32_t *__restrict__ lens, uint64_t lead, uint64_t n,
                                                      uint32_t *__restrict__ out, const uint32_t *__restrict__ gtab,
-                                                     uint32_t *__restrict__ status) {
+                                                     uint32_t *__restrict__ status, const RangeDesc *__restrict__ gate,
+                                                     uint32_t ngate) {
     typedef const __attribute__((address_space(1))) uint64_t gu64;
     typedef const __attribute__((address_space(1))) uint32_t gu32;
+    // Fallback of launch_packed_ranges: runs only if a piece sub-launch found a packet
+    // outside its view (the offsets were not packed); then it redoes the whole batch.
+    if (gate) {
+        uint32_t any = 0;
+        for (uint32_t j = 0; j < ngate; ++j) any |= gate[j].bad;
+        if (!any) return;
+    }
     __shared__ __attribute__((aligned(16))) uint32_t lds_w[kStLdsWords];
     char *lds = reinterpret_cast<char *>(lds_w);
     const uint64_t g0 = n * blockIdx.x / gridDim.x, g1 = n * (blockIdx.x + 1) / gridDim.x;
@@ -2202,14 +2285,14 @@ int launch_pieces(DevState &s, const uint8_t *base, uint64_t nbytes, Prov prov, 
 // Packed mixed lengths (k_stream): one launch for any n and any buffer size (64-bit
 // offsets, per-round buffer resources); the kernel finds its own workgroup ranges.
 int launch_stream(DevState &s, const uint8_t *base, uint64_t nbytes, const uint64_t *offs, const uint32_t *lens,
-                  uint64_t n, uint32_t *out, hipStream_t st) {
+                  uint64_t n, uint32_t *out, hipStream_t st, const dev::RangeDesc *gate = nullptr, uint32_t ngate = 0) {
     const uint64_t lead = reinterpret_cast<uintptr_t>(base) & 15u;
     uint64_t grid = (n + dev::kStWaves * 64 - 1) / (dev::kStWaves * 64);  // >= 64 payloads per wave
     if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
     if (grid == 0) grid = 1;
     note_kernel("k_stream");
     hipLaunchKernelGGL((dev::k_stream<0>), dim3(unsigned(grid)), dim3(dev::kStThreads), 0, st, base - lead,
-                       lead + nbytes, offs, lens, lead, n, out, s.tabs, s.status);
+                       lead + nbytes, offs, lens, lead, n, out, s.tabs, s.status, gate, ngate);
     return launch_check("k_stream");
 }
 
@@ -2267,6 +2350,119 @@ struct ArrayProvL {
         ok = true;
     }
 };
+// Packed batches >= 2 GiB (launch_packed_ranges): ArrayProvL over one device-bound
+// sub-range of the arrays (RangeDesc), 64-bit offsets rebased onto the sub-launch's
+// < 2 GiB view.  A packet outside the view (offsets not packed) is flagged, not read.
+struct RangeArrayProvL {
+    static constexpr const char *kName = "RangeArrayProvL";  // wtp_last_kernel()
+    static constexpr bool kVarLen = true;
+    static constexpr bool kIndexed = false;
+    static constexpr bool kGroupLoad = true;
+    static constexpr bool kDevRange = true;
+    const uint64_t *__restrict__ offs;  // the caller's arrays (bind() moves them to the range)
+    const uint32_t *__restrict__ lens;
+    RangeDesc *desc;
+    uint64_t lead;        // the caller's base mod 16
+    uint64_t rebase = 0;  // bind(): view offset of this launch's resource base
+    uint32_t n = 0, vbytes = 0;
+    template <class E>
+    __device__ __forceinline__ bool bind(const uint8_t *&base, uint32_t &nbytes, uint64_t &nn, E &e) {
+        const uint64_t b = desc->begin, en = desc->end;
+        if (b >= en || desc->bad) return false;
+        rebase = desc->rebase;
+        vbytes = desc->nbytes;
+        offs += b;
+        lens += b;
+        n = uint32_t(en - b);  // <= kSubBatch
+        base += rebase;
+        nbytes = vbytes;
+        nn = en - b;
+        e.rebase(b, n);
+        return true;
+    }
+    __device__ __forceinline__ void flag_outside() const { atomicOr(&desc->bad, 1u); }
+    __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
+        r.a = offs[p];
+        r.b = lens[p];
+    }
+    __device__ __forceinline__ void load_group(uint64_t q0, uint32_t lane, MetaRaw &r) const {
+        const uint32_t pi = uint32_t(q0) + lane;  // past n: 0
+        const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(make_rsrc(offs, n * 8u),
+                                                                                        int(pi * 8u), 0, 0));
+        r.a = uint64_t(w.x) | (uint64_t(w.y) << 32);
+        r.b = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(lens, n * 4u), int(pi * 4u), 0, 0);
+    }
+    __device__ __forceinline__ uint32_t load_len(uint64_t p) const { return lens[p]; }
+    __device__ __forceinline__ const uint32_t *len_array() const { return lens; }
+    __device__ __forceinline__ uint32_t len_of(uint32_t w) const { return w; }
+    __device__ __forceinline__ void decode(const MetaRaw &r, uint64_t &off, uint32_t &l, bool &ok, uint32_t &,
+                                           uint32_t &) const {
+        const uint64_t o = r.a + lead - rebase;  // offset in this launch's view (mod 2^64)
+        const bool in = o <= uint64_t(vbytes) && uint64_t(r.b) <= uint64_t(vbytes) - o;
+        off = in ? o : 0u;
+        l = in ? r.b : 0u;
+        ok = in;
+    }
+};
+
+// Sub-ranges of a packed batch for launch_packed_ranges: cuts where the view offset
+// reaches k * G (binary search over the offsets; a prefix max keeps them monotone for
+// any offsets) merged with the count cuts j * sb, so every range holds <= sb packets
+// and, if packed, its bytes lie within G + 4 KiB < 2 GiB of its first offset.
+constexpr uint32_t kMaxRanges = 1024;
+__global__ __launch_bounds__(256) void k_cut_ranges(const uint64_t *__restrict__ offs, uint64_t n, uint64_t lead,
+                                                    uint64_t vspan, uint64_t G, uint32_t kb, uint64_t sb,
+                                                    RangeDesc *__restrict__ desc, uint32_t nd) {
+    __shared__ uint64_t bcut[kMaxRanges];
+    __shared__ uint64_t cuts[kMaxRanges + 1];
+    for (uint32_t k = threadIdx.x + 1; k < kb; k += blockDim.x) {
+        const uint64_t t = uint64_t(k) * G;
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t m = lo + (hi - lo) / 2;
+            if (offs[m] + lead < t) lo = m + 1;
+            else hi = m;
+        }
+        bcut[k] = lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t pb = 0, jc = sb;
+        uint32_t k = 1, m = 1;
+        cuts[0] = 0;
+        while (m < nd) {
+            const uint64_t b = k < kb ? (bcut[k] > pb ? bcut[k] : pb) : ~0ull;
+            const uint64_t c = jc < n ? jc : ~0ull;
+            if (b <= c) {
+                cuts[m++] = b;
+                pb = b;
+                ++k;
+            } else {
+                cuts[m++] = c;
+                jc += sb;
+            }
+        }
+        cuts[nd] = n;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+        RangeDesc d{};
+        d.begin = cuts[j];
+        d.end = cuts[j + 1] > cuts[j] ? cuts[j + 1] : cuts[j];
+        d.nbytes = 16;
+        if (d.begin < d.end) {
+            const uint64_t r = (offs[d.begin] + lead) & ~uint64_t(15);
+            if (r < vspan) {
+                d.rebase = r;
+                d.nbytes = uint32_t(vspan - r < (1ull << 31) - 16 ? vspan - r : (1ull << 31) - 16);
+            } else {
+                d.bad = 1;  // an offset past the buffer: not a packed batch
+            }
+        }
+        desc[j] = d;
+    }
+}
+
 // Datagram p = view[lead + p*stride, +recv_len[p]): header (16 B) + payload.  aux =
 // ntohl(header.checksum): the two dwords covering header bytes 12..15 ride with the
 // metadata prefetch (through the view's buffer resource: the second dword may lie past
@@ -2300,6 +2496,49 @@ struct DgramProvL {
     }
 };
 }  // namespace dev
+
+namespace {
+// Packed mixed lengths in a buffer >= 2 GiB (wtp_crc32_batch_packed): the piece kernel in
+// sub-launches over < 2 GiB views instead of k_stream (C5-like data: 43 vs 57 us per 1 M
+// packets).  The host knows neither offsets nor lengths, so the cuts are
+// made on the device (k_cut_ranges: view offsets at multiples of G, packet counts at
+// multiples of kSubBatch) and each k_pieces sub-launch binds its range from its
+// descriptor (RangeArrayProvL); the host launches an upper bound of kb + nc - 1 of them
+// (empty ones return at once).  Exact for any offsets: a sub-launch that meets a packet
+// outside its view flags its descriptor, and the gated k_stream launch at the end then
+// recomputes the whole batch (it returns at once otherwise).  Asynchronous on `st`; the
+// descriptors come from the library's stream-ordered pool.
+int launch_packed_ranges(DevState &s, const uint8_t *b, uint64_t base_bytes, const uint64_t *offs,
+                         const uint32_t *lens, uint64_t n, uint32_t *out, hipStream_t st) {
+    const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
+    const uint8_t *view = b - lead;
+    const uint64_t vspan = (lead + base_bytes + 15) & ~uint64_t(15);
+    constexpr uint64_t G = (1ull << 31) - (1ull << 16);  // packed: a range spans <= G + 4111 B < 2 GiB - 16
+    const uint64_t kb = (vspan + G - 1) / G, nc = (n + kSubBatch - 1) / kSubBatch;
+    const uint64_t nd = kb + nc - 1;
+    if (nd > dev::kMaxRanges) return launch_stream(s, b, base_bytes, offs, lens, n, out, st);
+    dev::RangeDesc *d = nullptr;
+    WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&d), nd * sizeof(dev::RangeDesc), s.pool, st));
+    int rc = WTP_OK;
+    hipLaunchKernelGGL(dev::k_cut_ranges, dim3(1), dim3(256), 0, st, offs, n, lead, vspan, G, uint32_t(kb),
+                       uint64_t(kSubBatch), d, uint32_t(nd));
+    rc = launch_check("k_cut_ranges");
+    const uint64_t per = n < kSubBatch ? n : kSubBatch;  // packets of the largest range: the grid
+    uint64_t grid = ((per + 63) / 64 + dev::kPcThreads / 64 - 1) / (dev::kPcThreads / 64);
+    if (grid > uint64_t(s.grid_cus())) grid = uint64_t(s.grid_cus());
+    for (uint64_t j = 0; j < nd && !rc; ++j) {
+        hipLaunchKernelGGL((dev::k_pieces<dev::RangeArrayProvL, dev::CrcEpi>), dim3(unsigned(grid)),
+                           dim3(dev::kPcThreads), 0, st, view, uint32_t(0),
+                           dev::RangeArrayProvL{offs, lens, d + j, lead}, per, dev::CrcEpi{out, 0}, s.tabs, s.status);
+        rc = launch_check("k_pieces");
+    }
+    if (!rc) rc = launch_stream(s, b, base_bytes, offs, lens, n, out, st, d, uint32_t(nd));
+    note_kernel("k_pieces<RangeArrayProvL, CrcEpi> x %llu (+ k_stream if not packed)", (unsigned long long)nd);
+    const hipError_t fe = hipFreeAsync(d, st);
+    if (!rc && fe != hipSuccess) rc = fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
+    return rc;
+}
+}  // namespace
 
 }  // namespace wtp
 
@@ -2415,15 +2654,22 @@ int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t
                            const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream) {
     if (n == 0) return WTP_OK;
     if (!d_base || !d_offsets || !d_lengths || !d_out) return fail(WTP_EINVAL, "null pointer");
-    // Below 2 GiB the piece-stream kernel is the faster one on every distribution measured
-    // (C5 Zipf 1.1: 45.6 vs 57.0 us), so a packed batch takes the same route as
-    // wtp_crc32_batch_var; WTP_STREAM_KERNEL=1 in the environment forces the stream
-    // kernel (tests, measurements).
+    // The piece-stream kernel is the faster one on every distribution measured (C5 Zipf
+    // 1.1: 45.6 vs 57.0 us), so below 2 GiB a packed batch takes the same route as
+    // wtp_crc32_batch_var, and from 2 GiB on it runs the same kernel in < 2 GiB
+    // sub-launches cut on the device (launch_packed_ranges).  WTP_STREAM_KERNEL=1 in the
+    // environment forces the stream kernel (tests, measurements).
     const char *force = getenv("WTP_STREAM_KERNEL");
-    if (!(force && force[0] == '1')) return wtp_crc32_batch_var(d_base, base_bytes, d_offsets, d_lengths, n, d_out, stream);
+    const bool stream_kernel = force && force[0] == '1';
+    const uint64_t lead = reinterpret_cast<uintptr_t>(d_base) & 15u;
+    const bool big = ((lead + base_bytes + 15) & ~uint64_t(15)) >= (1ull << 31);
+    if (!stream_kernel && !big) return wtp_crc32_batch_var(d_base, base_bytes, d_offsets, d_lengths, n, d_out, stream);
     DevState *s = nullptr;
     int rc = current(s);
     if (rc) return rc;
+    if (!stream_kernel)
+        return launch_packed_ranges(*s, static_cast<const uint8_t *>(d_base), base_bytes, d_offsets, d_lengths, n,
+                                    d_out, static_cast<hipStream_t>(stream));
     return launch_stream(*s, static_cast<const uint8_t *>(d_base), base_bytes, d_offsets, d_lengths, n, d_out,
                          static_cast<hipStream_t>(stream));
 }

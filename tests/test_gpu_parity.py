@@ -648,6 +648,44 @@ def test_packed_view_over_4gib(W, VAR):
     del d
 
 
+@pytest.mark.parametrize("broken", [False, True])
+def test_packed_zipf_over_2gib_piece_ranges(W, broken):
+    """wtp_crc32_batch_packed on 17 M Zipf(1.1) payloads (2.3 GB, past 2 GiB): the piece
+    kernel in device-cut < 2 GiB sub-launches (launch_packed_ranges), not k_stream.  Every
+    CRC equals the stream kernel's over the same batch (WTP_STREAM_KERNEL=1) and the oracle
+    on the payloads around each 2 GiB - 64 KiB cut and a random sample.  broken: 40 pairs of
+    payloads swapped (offsets not packed) -> a sub-launch flags them and the gated k_stream
+    recomputes the batch; still exact."""
+    n = 17_000_000
+    lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
+    offs, lens = _packed(lens, first=3)
+    rng = np.random.default_rng(17)
+    if broken:
+        for b in np.sort(rng.choice(n - 2, 40, replace=False)):
+            offs[[b, b + 1]] = offs[[b + 1, b]]
+            lens[[b, b + 1]] = lens[[b + 1, b]]
+    total = int((offs + lens).max()) + 8
+    assert total > (1 << 31)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = u32_out(n)
+    W.crc32_batch_packed(d, total, do, dl, n, out)
+    assert W.LIB.wtp_last_kernel().decode().startswith("k_pieces<RangeArrayProvL, CrcEpi>")
+    got = to_u32(out, n)
+    ref = u32_out(n)
+    _forced_stream(W)(d, total, do, dl, n, ref)
+    assert np.array_equal(got, to_u32(ref, n))
+    G = (1 << 31) - (1 << 16)
+    cut = int(np.searchsorted(offs, np.uint64(G - 3)))
+    idx = np.unique(np.concatenate([np.arange(cut - 3, cut + 3), [0, n - 1], rng.integers(0, n, 3000)]))
+    host = d.cpu().numpy()
+    del d
+    want = O.batch_var(host, offs[idx], lens[idx])
+    assert np.array_equal(got[idx], want)
+
+
 def test_var_unordered_view_over_2gib(W):
     """wtp_crc32_batch_var on a 2.3 GB buffer (no longer EINVAL): 100 K payloads at
     unordered, overlapping offsets across the whole buffer, lengths 0..1500 and a few

@@ -234,6 +234,49 @@ def c5(s, entry="var"):
             "parity_all": ok}
 
 
+def c5big(s=1.1, n=17_000_000):
+    """C5's distribution in a packed buffer past 2 GiB (17 M payloads, ~2.3 GB): the piece
+    kernel in device-cut < 2 GiB sub-launches (wtp_crc32_batch_packed) against k_stream
+    (wtp_crc32_batch_var, which takes it there, and the forced packed route).  The routes'
+    vectors must be equal; a sample of 4000 payloads is checked against the oracle."""
+    lens = O.zipf_lengths(n, s=s)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    d = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d, nbytes=total)
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    rb = total + 12 * n
+    rows, vecs = [], {}
+    for entry in ("packed", "var"):
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        fn = W.crc32_batch_packed if entry == "packed" else W.crc32_batch_var
+        f = lambda: fn(d, total, do, dl, n, out)  # noqa: E731
+        med, mean = timed(f, 20)
+        try:  # the packed route allocates its descriptors from a stream-ordered pool
+            gl, _ = graph_time(f, G=5, reps=5, per=4)
+        except Exception as e:  # noqa: BLE001 — reported, not fatal
+            gl, gerr = float("nan"), f"{e.__class__.__name__}: {e}"[:200]
+        else:
+            gerr = None
+        kern = W.LIB.wtp_last_kernel().decode()
+        vecs[entry] = out.cpu().numpy().view(np.uint32).copy()
+        rows.append({"config": f"C5 distribution past 2 GiB: {n} packed payloads Zipf(s={s}), "
+                               f"wtp_crc32_batch_{entry} -> {kern}", "packets": n, "payload_bytes": total,
+                     "read_bytes_incl_meta": rb, "ms_per_launch": round(mean, 4),
+                     "read_GBps": round(rb / (mean * 1e-3) / GB, 1), "frac_hbm": round(rb / (mean * 1e-3) / GB / PEAK, 4),
+                     "graph_ms_per_launch": round(gl, 4), "graph_frac_hbm": round(rb / (gl * 1e-3) / GB / PEAK, 4),
+                     "graph_error": gerr})
+    idx = np.random.default_rng(5).integers(0, n, 4000)
+    host = d.cpu().numpy()
+    del d
+    ok = bool(np.array_equal(vecs["packed"], vecs["var"])) and bool(
+        np.array_equal(vecs["packed"][idx], O.batch_var(host, offs[idx], lens[idx])))
+    for r in rows:
+        r["parity_routes_equal_and_sample"] = ok
+    return rows
+
+
 def verify():
     n, stride = 1 << 20, 1472
     wire = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
@@ -387,6 +430,8 @@ def main():
     if "c5" in sel:
         for entry in ("stream", "var", "packed"):
             add(c5(1.1, entry), c5(1.0, entry))
+    if "c5big" in sel:
+        add(*c5big())
     if "verify" in sel:
         add(*verify())
     if "c3" in sel:

@@ -59,6 +59,14 @@ for s in $STEPS; do
              cd "$ROOT"
            done
            python3 tools/sq_json.py "$OUT/c5_counters.json" $(for lib in ${SQ_LIBS:-product}; do echo "$lib=$OUT/sq_$lib"; done) > "$OUT/sq_json.log" 2>&1 || true ;;
+    c5fetch) for lib in ${SQ_LIBS:-product}; do  # FETCH_SIZE of the C5 launch, one pass per library build
+             if [ "$lib" = product ]; then LP="$ROOT/a3-reliable-transport_amd/lib/libwtp_crc32.so"; else LP="$ROOT/a3-reliable-transport_amd/lib/ab/$lib.so"; fi
+             cd /tmp
+             WTP_LIB="$LP" run "fetch_$lib" 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$lib" -o c5 \
+               -- python3 "$ROOT/tools/prof_pieces.py" 5
+             cd "$ROOT"
+           done
+           python3 tools/c5_fetch_summary.py "$OUT/c5_fetch.json" $(for lib in ${SQ_LIBS:-product}; do echo "$lib=$OUT/fetch_$lib"; done) > "$OUT/c5_fetch.log" 2>&1 || true ;;
     profwin) python3 tools/rocprof_window.py $(find "$OUT/prof" -name "*kernel_trace.csv" | head -1) "k_fixed_braid<6" 20 \
                "$OUT/rocprof_timed_window.json" $(python3 -c "import json,sys;print([json.loads(l) for l in open('$OUT/prof.log') if l.startswith('{')][-1]['warmup_run'])") > "$OUT/profwin.log" 2>&1 || true ;;
     tests) # a stale PMC record (the shipped k_fixed_braid<6> code differs from the one it measured)
