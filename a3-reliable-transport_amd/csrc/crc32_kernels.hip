@@ -1124,13 +1124,18 @@ struct SpanDma {
     __device__ __forceinline__ static void wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 
+// Maximum over the wave (unsigned; 0 is neutral), by the same DPP steps as wave_incl_add
+// (a __shfl_xor ladder here changed how the compiler lowered the loop's other
+// shuffles and cost C5 ~2 us per launch).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t u = uint32_t(__shfl_xor(int(v), o));
-        v = u > v ? u : v;
-    }
-    return uint32_t(__builtin_amdgcn_readfirstlane(int(v)));
+    auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xF, 0xF, false)));
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xF, 0xF, false)));
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xF, 0xF, false)));
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xF, 0xF, false)));
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xA, 0xF, false)));
+    v = mx(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xC, 0xF, false)));
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
 }
 
 // Tail clamp of the span prefetch: a wave's last rounds used to prefetch a full 4352-B
@@ -1140,7 +1145,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // (tools/c5_span_model.py, profiles/r05).  When the round's view holds every packet the
 // wave has left, the prefetch stops at the end of the last of them.
 #ifndef WTP_PC_TAILCLAMP
-#define WTP_PC_TAILCLAMP 1
+#define WTP_PC_TAILCLAMP 0  // measured and not shipped: -12.1 MB of reads, +1.5 us
 #endif
 
 // The wave's packets form one stream of 64-B pieces (each packet cut into pieces counted
@@ -1532,7 +1537,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 // compile error, not a library that runs wrong.
 #ifndef WTP_AB_BUILD
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1 &&
-                  WTP_PC_TAILCLAMP == 1,
+                  WTP_PC_TAILCLAMP == 0,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
 static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 0,
@@ -2094,6 +2099,13 @@ struct DevState {
     std::atomic<int> reserve{0};  // CUs left free of the persistent kernels (wtp_reserve_cus)
     unsigned grid_cus() const { return unsigned(std::max(1, cus - reserve.load(std::memory_order_relaxed))); }
     hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed (builder scratch)
+    // Per-stream device scratch of fixed size (launch_packed_ranges' descriptors): made on
+    // a stream's first use outside graph capture and kept, so calls captured into a graph
+    // bake in a buffer that outlives the graph.  (Stream-ordered pool allocations inside a
+    // capture replayed wrongly when one graph held several calls: the sub-launches read
+    // zeroed descriptors and did nothing; profiles/r05)
+    std::mutex smu;
+    std::unordered_map<hipStream_t, void *> sbuf;
 };
 constexpr int kMaxDev = 64;
 DevState g_dev[kMaxDev];
@@ -2172,6 +2184,27 @@ int current(DevState *&s) {
     int rc = init_device(dev);
     if (rc) return rc;
     s = &g_dev[dev];
+    return WTP_OK;
+}
+
+// The stream's scratch buffer (kStreamScratch bytes), made on first use.  A first use
+// while the stream is capturing a graph is an error (no allocation may happen there).
+constexpr size_t kStreamScratch = 32768;
+int stream_scratch(DevState &s, hipStream_t st, void **out) {
+    std::lock_guard<std::mutex> g(s.smu);
+    auto it = s.sbuf.find(st);
+    if (it != s.sbuf.end()) {
+        *out = it->second;
+        return WTP_OK;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    WTP_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(WTP_EINVAL, "packed batch >= 2 GiB: the stream's first such call must run outside graph capture");
+    void *p = nullptr;
+    WTP_HIP(hipMalloc(&p, kStreamScratch));
+    s.sbuf.emplace(st, p);
+    *out = p;
     return WTP_OK;
 }
 
@@ -2507,7 +2540,8 @@ namespace {
 // (empty ones return at once).  Exact for any offsets: a sub-launch that meets a packet
 // outside its view flags its descriptor, and the gated k_stream launch at the end then
 // recomputes the whole batch (it returns at once otherwise).  Asynchronous on `st`; the
-// descriptors come from the library's stream-ordered pool.
+// descriptors live in the stream's scratch (stream_scratch: calls on one stream are
+// ordered, so they may share it).
 int launch_packed_ranges(DevState &s, const uint8_t *b, uint64_t base_bytes, const uint64_t *offs,
                          const uint32_t *lens, uint64_t n, uint32_t *out, hipStream_t st) {
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
@@ -2517,9 +2551,10 @@ int launch_packed_ranges(DevState &s, const uint8_t *b, uint64_t base_bytes, con
     const uint64_t kb = (vspan + G - 1) / G, nc = (n + kSubBatch - 1) / kSubBatch;
     const uint64_t nd = kb + nc - 1;
     if (nd > dev::kMaxRanges) return launch_stream(s, b, base_bytes, offs, lens, n, out, st);
+    static_assert(dev::kMaxRanges * sizeof(dev::RangeDesc) <= kStreamScratch, "descriptor scratch");
     dev::RangeDesc *d = nullptr;
-    WTP_HIP(hipMallocFromPoolAsync(reinterpret_cast<void **>(&d), nd * sizeof(dev::RangeDesc), s.pool, st));
-    int rc = WTP_OK;
+    int rc = stream_scratch(s, st, reinterpret_cast<void **>(&d));
+    if (rc) return rc;
     hipLaunchKernelGGL(dev::k_cut_ranges, dim3(1), dim3(256), 0, st, offs, n, lead, vspan, G, uint32_t(kb),
                        uint64_t(kSubBatch), d, uint32_t(nd));
     rc = launch_check("k_cut_ranges");
@@ -2534,8 +2569,6 @@ int launch_packed_ranges(DevState &s, const uint8_t *b, uint64_t base_bytes, con
     }
     if (!rc) rc = launch_stream(s, b, base_bytes, offs, lens, n, out, st, d, uint32_t(nd));
     note_kernel("k_pieces<RangeArrayProvL, CrcEpi> x %llu (+ k_stream if not packed)", (unsigned long long)nd);
-    const hipError_t fe = hipFreeAsync(d, st);
-    if (!rc && fe != hipSuccess) rc = fail(WTP_EHIP, "hipFreeAsync: %s", hipGetErrorString(fe));
     return rc;
 }
 }  // namespace
@@ -2637,10 +2670,11 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
     const uint64_t lead = reinterpret_cast<uintptr_t>(b) & 15u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     // The general kernel addresses a view of < 2 GiB (32-bit buffer offsets).  Larger
-    // buffers go to the stream kernel, which takes 64-bit offsets: packed runs on its
-    // fast path, any other layout on its lane-per-payload path, exact either way.
+    // buffers take launch_packed_ranges: device-cut < 2 GiB sub-launches of the same
+    // kernel when the offsets are packed (the common layout even through this entry),
+    // else the gated stream kernel (64-bit offsets, exact for any layout) redoes the batch.
     if (((lead + base_bytes + 15) & ~uint64_t(15)) >= (1ull << 31))
-        return launch_stream(*s, b, base_bytes, d_offsets, d_lengths, n, d_out, st);
+        return launch_packed_ranges(*s, b, base_bytes, d_offsets, d_lengths, n, d_out, st);
     for (uint64_t p = 0; p < n; p += kSubBatch) {
         const uint64_t cnt = std::min<uint64_t>(kSubBatch, n - p);
         rc = launch_pieces(*s, b, base_bytes, dev::ArrayProvL{d_offsets + p, d_lengths + p, lead, uint32_t(cnt)}, cnt,

@@ -104,9 +104,10 @@ int wtp_crc32_batch_fixed(const void *d_payloads, size_t stride, size_t len, siz
 
 /* Mixed lengths: payload i = d_base[d_offsets[i] .. d_offsets[i] + d_lengths[i]), any
    order, overlaps allowed.  `base_bytes` = size of the d_base buffer (bounds for the
-   loads).  Buffers below 2 GiB run the general (piece-stream) kernel; larger ones run
-   the stream kernel of wtp_crc32_batch_packed (64-bit offsets), so there is no size
-   limit.  d_lengths[i] <= WTP_MAX_KERNEL_LEN. */
+   loads).  Buffers below 2 GiB run the general (piece-stream) kernel; larger ones take
+   the route of wtp_crc32_batch_packed there (the piece kernel in device-cut < 2 GiB
+   sub-launches, and the stream kernel, 64-bit offsets, for batches whose offsets turn
+   out not to be packed), so there is no size limit.  d_lengths[i] <= WTP_MAX_KERNEL_LEN. */
 int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                         const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
@@ -118,10 +119,16 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
    Payloads that break the packing, or are longer than 4095 B, are still computed
    exactly on a slower lane-per-payload path, so results are correct for any offsets;
    lengths > WTP_MAX_KERNEL_LEN give crc 0 and set the status flag.
-   The library picks the kernel: below 2 GiB the general kernel, currently the faster
-   one on packed batches too (C5: DESIGN.md), so this call then equals
-   wtp_crc32_batch_var; at or above 2 GiB the stream kernel (which wtp_crc32_batch_var
-   also uses there).  WTP_STREAM_KERNEL=1 in the environment forces the stream kernel. */
+   The library picks the kernel: below 2 GiB the general kernel, the faster one on
+   packed batches too (C5: DESIGN.md), so this call then equals wtp_crc32_batch_var; at
+   or above 2 GiB the general kernel in sub-launches over < 2 GiB views that the device
+   cuts from the offsets; a sub-launch that meets a payload outside its
+   view (offsets not packed) flags it and the stream kernel then recomputes the batch,
+   so results stay exact for any offsets.  That route keeps 32 KiB of device scratch per
+   stream, made on the stream's first such call, which must not be inside a graph
+   capture (a captured call reuses it: replay such a graph only where no other call of
+   this route runs on its capture stream at the same time).  WTP_STREAM_KERNEL=1 in the
+   environment forces the stream kernel. */
 int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 

@@ -686,6 +686,80 @@ def test_packed_zipf_over_2gib_piece_ranges(W, broken):
     assert np.array_equal(got[idx], want)
 
 
+def _graph_of(calls):
+    """One HIP graph holding `calls` in order, captured on a side stream after one eager
+    run of each there (library state keyed by stream is made outside the capture)."""
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        for c in calls:
+            c()
+    cs.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cs):
+        for c in calls:
+            c()
+    return g
+
+
+def test_packed_over_2gib_graph_of_three_calls(W):
+    """Three packed >= 2 GiB calls (device-cut piece sub-launches) captured in ONE graph,
+    each into its own output: after clearing, a replay rewrites all three, equal to the
+    eager results, and a copy queued behind the replay sees them (stream order).  With
+    descriptors from a stream-ordered pool, such a graph replayed as no-ops (r05b)."""
+    n = 17_000_000
+    lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
+    offs, lens = _packed(lens)
+    total = int(offs[-1] + lens[-1])
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    outs = [u32_out(n) for _ in range(3)]
+    calls = [lambda o=o: W.crc32_batch_packed(d, total, do, dl, n, o) for o in outs]
+    calls[0]()
+    want = outs[0].clone()
+    g = _graph_of(calls)
+    torch.cuda.synchronize()
+    for o in outs:
+        o.zero_()
+    g.replay()
+    snap = torch.stack(outs).clone()  # queued behind the replay, no host sync in between
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert torch.equal(snap[i], want), i
+    idx = np.random.default_rng(3).integers(0, n, 500)
+    host_idx = np.unique(idx)
+    got = to_u32(outs[2], n)
+    for i in host_idx[:50]:
+        i = int(i)
+        assert int(got[i]) == O.crc32(d[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy()), i
+
+
+def test_builder_slow_path_graph_of_three_calls(W):
+    """The fused builder's three-step path (unaligned payloads, no length array: its CRCs
+    go through stream-ordered scratch) three times in ONE graph, each into its own wire
+    buffer: a replay after clearing rebuilds all three exactly as the eager calls did."""
+    m = 20_001
+    pay = torch.empty(m * 1456 + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(pay)
+    wires = [torch.zeros(m * 1472 + 64, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    calls = [lambda w=w, k=k: W.build_data_packets(pay[3 + k:], m * 1456 - 100, 7, w, 1472, None)
+             for k, w in enumerate(wires)]
+    for c in calls:
+        c()
+    torch.cuda.synchronize()
+    want = [w.clone() for w in wires]
+    g = _graph_of(calls)
+    torch.cuda.synchronize()
+    for w in wires:
+        w.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for k in range(3):
+        assert torch.equal(wires[k], want[k]), k
+
+
 def test_var_unordered_view_over_2gib(W):
     """wtp_crc32_batch_var on a 2.3 GB buffer (no longer EINVAL): 100 K payloads at
     unordered, overlapping offsets across the whole buffer, lengths 0..1500 and a few

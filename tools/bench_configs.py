@@ -236,9 +236,10 @@ def c5(s, entry="var"):
 
 def c5big(s=1.1, n=17_000_000):
     """C5's distribution in a packed buffer past 2 GiB (17 M payloads, ~2.3 GB): the piece
-    kernel in device-cut < 2 GiB sub-launches (wtp_crc32_batch_packed) against k_stream
-    (wtp_crc32_batch_var, which takes it there, and the forced packed route).  The routes'
-    vectors must be equal; a sample of 4000 payloads is checked against the oracle."""
+    kernel in device-cut < 2 GiB sub-launches (wtp_crc32_batch_packed, and
+    wtp_crc32_batch_var, which takes the same route there) against k_stream (forced, the
+    route of both before round 5).  The routes' vectors must be equal; a sample of 4000
+    payloads is checked against the oracle."""
     lens = O.zipf_lengths(n, s=s)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.sum())
@@ -248,9 +249,11 @@ def c5big(s=1.1, n=17_000_000):
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     rb = total + 12 * n
     rows, vecs = [], {}
-    for entry in ("packed", "var"):
+    for entry in ("packed", "var", "stream"):
         out = torch.empty(n, dtype=torch.int32, device="cuda")
-        fn = W.crc32_batch_packed if entry == "packed" else W.crc32_batch_var
+        if entry == "stream":  # the stream kernel, forced (the route both entries took before round 5)
+            os.environ["WTP_STREAM_KERNEL"] = "1"
+        fn = W.crc32_batch_var if entry == "var" else W.crc32_batch_packed
         f = lambda: fn(d, total, do, dl, n, out)  # noqa: E731
         med, mean = timed(f, 20)
         try:  # the packed route allocates its descriptors from a stream-ordered pool
@@ -260,6 +263,7 @@ def c5big(s=1.1, n=17_000_000):
         else:
             gerr = None
         kern = W.LIB.wtp_last_kernel().decode()
+        os.environ.pop("WTP_STREAM_KERNEL", None)
         vecs[entry] = out.cpu().numpy().view(np.uint32).copy()
         rows.append({"config": f"C5 distribution past 2 GiB: {n} packed payloads Zipf(s={s}), "
                                f"wtp_crc32_batch_{entry} -> {kern}", "packets": n, "payload_bytes": total,
@@ -270,7 +274,7 @@ def c5big(s=1.1, n=17_000_000):
     idx = np.random.default_rng(5).integers(0, n, 4000)
     host = d.cpu().numpy()
     del d
-    ok = bool(np.array_equal(vecs["packed"], vecs["var"])) and bool(
+    ok = bool(np.array_equal(vecs["packed"], vecs["var"])) and bool(np.array_equal(vecs["packed"], vecs["stream"])) and bool(
         np.array_equal(vecs["packed"][idx], O.batch_var(host, offs[idx], lens[idx])))
     for r in rows:
         r["parity_routes_equal_and_sample"] = ok
