@@ -721,7 +721,7 @@ def main():
     kmean = sum(kern_ms) / len(kern_ms)
 
     per_rank = None
-    if world > 1:
+    if world > 1 or args.gather_n1:  # --gather-n1: the same fields from a one-rank RCCL world
         el, per_rank = rank_fields(kern, pipe.gather_ms(), el, args.steps, world, dev)
 
     # parity of the WHOLE result vector (rank 0: the gathered vector when N > 1)

@@ -154,6 +154,10 @@ def test_bench_pipelined_gather_one_rank(W):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["config"]["gather"] and line["config"]["reserved_cus"] == 8
     assert line["parity"]["match"] is True, line["parity"]
+    # the N > 1 line's per-rank fields, here from RCCL collectives in a one-rank world
+    assert line["per_rank_kernel_ms"] == [line["kernel_ms_max_over_ranks"]] and line["kernel_ms_max_over_ranks"] > 0
+    assert line["gathers_per_rank"] == [3] and line["per_rank_gather_ms"][0] > 0  # 5 steps, pairs: 2 + flushed 1
+    assert abs(line["overlap"] - (line["step_ms"] - line["kernel_ms_max_over_ranks"])) < 1e-4
 
 
 def test_bench_c4_shard_gather_one_rank(W):
