@@ -2466,6 +2466,10 @@ __global__ __launch_bounds__(256) void k_cut_ranges(const uint64_t *__restrict__
         while (m < nd) {
             const uint64_t b = k < kb ? (bcut[k] > pb ? bcut[k] : pb) : ~0ull;
             const uint64_t c = jc < n ? jc : ~0ull;
+            if (b == ~0ull && c == ~0ull) {  // both lists used up (cannot happen for nd = kb + nc - 1): pad
+                cuts[m++] = n;
+                continue;
+            }
             if (b <= c) {
                 cuts[m++] = b;
                 pb = b;

@@ -363,3 +363,60 @@ def stream_wave(T: StreamTables, buf: bytes, offs, lens, view_addr: int = 0):
         R += ST_ROUND
         rounds += 1
     return out, rounds
+
+
+# ---- k_cut_ranges: sub-launches of a mixed-length batch past 2 GiB -----
+def cut_ranges(offs, n: int, lead: int, vspan: int, G: int, sb: int):
+    """Mirror of csrc/crc32_kernels.hip k_cut_ranges: byte cuts (first packet whose view
+    offset reaches k*G, binary search, prefix max) merged with count cuts j*sb; one
+    (begin, end, rebase, nbytes, bad) per sub-launch, kb + nc - 1 of them."""
+    kb = -(-vspan // G)
+    nc = -(-n // sb)
+    nd = kb + nc - 1
+    bcut = [0] * kb
+    for k in range(1, kb):
+        lo, hi, t = 0, n, k * G
+        while lo < hi:
+            m = lo + (hi - lo) // 2
+            if int(offs[m]) + lead < t:
+                lo = m + 1
+            else:
+                hi = m
+        bcut[k] = lo
+    cuts, pb, jc, k = [0], 0, sb, 1
+    while len(cuts) < nd:
+        b = max(bcut[k], pb) if k < kb else None
+        c = jc if jc < n else None
+        if b is None and c is None:
+            cuts.append(n)
+            continue
+        if c is None or (b is not None and b <= c):
+            cuts.append(b)
+            pb = b
+            k += 1
+        else:
+            cuts.append(c)
+            jc += sb
+    cuts.append(n)
+    out = []
+    for j in range(nd):
+        b, e = cuts[j], max(cuts[j + 1], cuts[j])
+        d = {"begin": b, "end": e, "rebase": 0, "nbytes": 16, "bad": 0}
+        if b < e:
+            r = (int(offs[b]) + lead) & ~15
+            if r < vspan:
+                d["rebase"], d["nbytes"] = r, min(vspan - r, (1 << 31) - 16)
+            else:
+                d["bad"] = 1
+        out.append(d)
+    return out
+
+
+def range_outside(d, offs, lens, lead: int):
+    """Packets of one sub-launch that RangeArrayProvL.decode puts outside its view."""
+    bad = []
+    for p in range(d["begin"], d["end"]):
+        o = int(offs[p]) + lead - d["rebase"]
+        if not (0 <= o <= d["nbytes"] and int(lens[p]) <= d["nbytes"] - o):
+            bad.append(p)
+    return bad

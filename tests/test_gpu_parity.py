@@ -686,6 +686,45 @@ def test_packed_zipf_over_2gib_piece_ranges(W, broken):
     assert np.array_equal(got[idx], want)
 
 
+def test_packed_over_2gib_edges_at_the_cut(W):
+    """The >= 2 GiB piece route's edges: a 4-B-misaligned base (d[5:]), a first offset
+    that is not 0, empty payloads and over-long (5000 B: crc 0, status flag) payloads right
+    at the 2 GiB - 64 KiB cut, a payload straddling it, and a short last range.  Every CRC
+    equal to the stream kernel's (forced) and the oracle around the cut."""
+    W.device_status(0, clear=True)
+    G = (1 << 31) - (1 << 16)
+    n = 1_650_000
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 2800, n).astype(np.uint32)
+    offs, lens = _packed(lens, first=7)
+    cut = int(np.searchsorted(offs + np.uint64(5), np.uint64(G)))  # view offsets include the base's lead
+    assert 100 < cut < n - 100
+    lens[cut - 3:cut - 1] = 0
+    lens[cut + 1] = 5000
+    lens[cut - 6] = 4096
+    offs, lens = _packed(lens, first=7)
+    total = int(offs[-1] + lens[-1]) + 3
+    assert total + 5 > (1 << 31) + (1 << 20)
+    d = torch.empty(total + 5, dtype=torch.uint8, device="cuda")
+    W.synth_fill(d)
+    dv = d[5:]
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    out, ref = u32_out(n), u32_out(n)
+    W.crc32_batch_packed(dv, total, do, dl, n, out)
+    assert W.LIB.wtp_last_kernel().decode().startswith("k_pieces<RangeArrayProvL")
+    assert W.device_status(0, clear=True) & 1  # the 5000-B payload
+    _forced_stream(W)(dv, total, do, dl, n, ref)
+    got = to_u32(out, n)
+    assert np.array_equal(got, to_u32(ref, n))
+    idx = np.arange(cut - 40, cut + 40)
+    host = d[5:].cpu().numpy()
+    del d, dv
+    want = O.batch_var(host, offs[idx], np.where(lens[idx] > 4096, 0, lens[idx]).astype(np.uint32))
+    assert np.array_equal(got[idx], want)
+    assert got[cut + 1] == 0 and got[cut - 3] == 0 and got[cut - 2] == 0
+
+
 def _graph_of(calls):
     """One HIP graph holding `calls` in order, captured on a side stream after one eager
     run of each there (library state keyed by stream is made outside the capture)."""

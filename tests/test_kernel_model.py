@@ -3,6 +3,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import kernel_model as KM
 from kernel_model import Tables, braid_crc, pieces_crc
 
 
@@ -85,3 +86,34 @@ def test_stream_model(case):
         buf = O.synth_fill_np(int(offs[-1] + lens[-1]) + 9, start_byte=first).tobytes()
         out, _ = K.stream_wave(T, buf, offs, lens, view_addr=view_addr)
         assert out == [O.crc32(buf[o:o + L]) for o, L in zip(offs, lens)], (case, first)
+
+
+@pytest.mark.parametrize("G,sb,lead", [(4096, 10**9, 0), (3000, 37, 5), (50_000, 100, 11), (1 << 20, 64, 3)])
+def test_cut_ranges_partition_and_views(G, sb, lead):
+    """k_cut_ranges (mirrored at small G and sub-batch sizes): the sub-launches partition
+    [0, n) in order, none holds more than sb packets, a packed batch's ranges each fit a
+    view of G + 4 KiB (nothing outside, so no fallback), and a batch with swapped payloads
+    still partitions, its out-of-view packets being exactly those the fallback must redo."""
+    rng = np.random.default_rng(G + sb)
+    n = 5000
+    lens = rng.integers(0, 4097, n).astype(np.int64)
+    lens[rng.integers(0, n, 200)] = 0
+    offs = np.concatenate([[3], 3 + np.cumsum(lens[:-1])]).astype(np.int64)
+    vspan = (lead + int(offs[-1] + lens[-1]) + 15) & ~15
+    for broken in (False, True):
+        o = offs.copy()
+        if broken:
+            for b in rng.choice(n - 1, 30, replace=False):
+                o[[b, b + 1]] = o[[b + 1, b]]
+        rs = KM.cut_ranges(o, n, lead, vspan, G, sb)
+        assert len(rs) == -(-vspan // G) + -(-n // sb) - 1
+        assert rs[0]["begin"] == 0 and rs[-1]["end"] == n
+        assert all(a["end"] == b["begin"] for a, b in zip(rs, rs[1:]))
+        assert all(r["end"] - r["begin"] <= sb for r in rs)
+        outside = [p for r in rs if r["begin"] < r["end"] for p in KM.range_outside(r, o, lens, lead)]
+        if not broken:
+            assert not outside and not any(r["bad"] for r in rs)
+            for r in rs:
+                if r["begin"] < r["end"]:
+                    end = max(int(o[p] + lens[p]) for p in range(r["begin"], r["end"])) + lead
+                    assert end - r["rebase"] <= G + 4096 + 16
