@@ -963,6 +963,29 @@ __device__ __forceinline__ uint32_t piece_count(const Prov &prov, uint64_t p) {
 #define WTP_PC_LAG 1  // k_pieces: wave priority by work left (0: rotate by round and age)
 #endif
 static_assert(kPcThreads >= 128 && kPcThreads <= 1024 && (kPcThreads & (kPcThreads - 1)) == 0, "k_pieces block");
+// Pieces of packets [p, min(p + 16, b)) from four 16-B length loads issued together (4-B
+// aligned offsets; words at or past g1 read 0 and are not counted).  Packets are taken
+// while the running count is below `want` (~0u: all; the boundary walk passes the pieces
+// left to its target), and *taken (if given) receives how many were.
+template <class Prov>
+__device__ __forceinline__ uint32_t chunk_pieces(const Prov &prov, uint64_t g1, uint64_t p, uint64_t b, uint32_t want,
+                                                 uint32_t *taken) {
+    const __amdgpu_buffer_rsrc_t lr = make_rsrc(prov.len_array(), uint32_t(4 * g1));
+    u32x4 q[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) q[j] = buf_ld16(lr, uint32_t(4 * (p + 4 * j)));
+    const uint32_t w[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
+                            q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+    uint32_t sum = 0, n = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        const bool step = p + i < b && sum < want;
+        sum += step ? pieces_of_len(prov.len_of(w[i])) : 0u;
+        n += step ? 1u : 0u;
+    }
+    if (taken) *taken = n;
+    return sum;
+}
 struct WaveSplit {
     static constexpr uint32_t kReg = 8, kThreads = kPcThreads, kWaves = kThreads / 64;
     uint32_t raw[kReg];  // length words of the first kReg packets of the sub-range
@@ -998,7 +1021,12 @@ struct WaveSplit {
             k[j] = j < m ? pieces_of_len(prov.len_of(raw[j])) : 0u;
             sum += k[j];
         }
-        for (uint64_t p = a + kReg; p < b; ++p) sum += piece_count(prov, p);  // > kReg per thread
+        // > kReg packets per thread (launches of more than 2 M packets): the rest in chunks
+        // of 16 length words, four 16-B loads in flight per chunk.  (A dword loop waited on
+        // each load: at 15 M packets per launch, ~50 serial loads here and up to ~57 in the
+        // boundary walk below cost ~0.1 ms per launch.)  Counts only balance the waves: the
+        // ranges stay a partition of [g0, g1) whatever they hold.
+        for (uint64_t p = a + kReg; p < b; p += 16) sum += chunk_pieces(prov, g1, p, b, ~0u, nullptr);
         const uint32_t incl = wave_incl_add(sum);
         uint32_t *const wsum = reinterpret_cast<uint32_t *>(lds + kPcBal);
         uint64_t *const starts = reinterpret_cast<uint64_t *>(lds + kPcBal + 64);
@@ -1028,7 +1056,11 @@ struct WaveSplit {
                     pre += step ? k[j] : 0u;
                     p += step ? 1u : 0u;
                 }
-                while (p < b && pre < target) pre += piece_count(prov, p++);
+                while (p < b && pre < target) {
+                    uint32_t taken = 0;
+                    pre += chunk_pieces(prov, g1, p, b, target - pre, &taken);
+                    p += taken;
+                }
                 starts[w] = p;
                 spre[w] = pre;
             }

@@ -369,6 +369,7 @@ def init_one_rank_group(local: int) -> None:
         s.close()
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")  # the gathers' own durations (Pipe.gather_ms)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
 
@@ -395,25 +396,16 @@ class Pipe:
         self.last_pos = 0
         self.timed = False  # time_steps sets it: the gathers issued meanwhile are timed
         self.gather_rec = []
-        self._obs = None    # side stream that waits for each timed gather (event mode)
 
     def _time_gather(self, work):
-        """Time one gather: from its inputs being ready (an event on the CRC stream, queued
-        right before the collective, i.e. after the step's CRC launch) to its completion on
-        the collective's stream (a side stream waits for the work, then records the end).
-        Without HIP streams (gloo CPU tests) the same span is taken on the host clock, from
-        the issue to the work's future completing."""
-        if hasattr(self.stream, "cuda_stream"):
-            import torch
-            if self._obs is None:
-                self._obs = torch.cuda.Stream()
-            end = TimingEvent()
-            with torch.cuda.stream(self._obs):
-                work.wait()
-                end.record(self._obs)
-            self.gather_rec[-1]["end"] = end
-        else:
-            rec = self.gather_rec[-1]
+        """Record one gather for gather_ms().  RCCL: the collective's own duration on its
+        stream, from ProcessGroupNCCL's start/end events (TORCH_NCCL_ENABLE_TIMING=1, which
+        main() sets before the process group exists; no extra stream or event of ours, so
+        nothing is queued beside the CRC stream's hardware queue).  gloo (CPU tests): the
+        host clock from the issue to the work's future completing."""
+        rec = self.gather_rec[-1]
+        rec["work"] = work
+        if not hasattr(self.stream, "cuda_stream"):
             rec["t0"] = time.perf_counter()
             work.get_future().then(lambda f, rec=rec: rec.__setitem__("t1", time.perf_counter()))
 
@@ -421,10 +413,16 @@ class Pipe:
         """Durations (ms) of the gathers issued while `timed` (call after drain())."""
         out = []
         for r in self.gather_rec:
-            if "end" in r:
-                out.append(r["start"].elapsed_time(r["end"]))
-            elif "t1" in r:
-                out.append((r["t1"] - r["t0"]) * 1e3)
+            d = None
+            if "t1" in r:
+                d = (r["t1"] - r["t0"]) * 1e3
+            elif "work" in r:
+                try:
+                    d = float(r["work"]._get_duration())
+                except Exception:  # noqa: BLE001 — timing not enabled / backend without it: not reported
+                    d = None
+            if d is not None:
+                out.append(d)
         return out
 
     def _group(self, pos):
@@ -452,11 +450,7 @@ class Pipe:
             half = self.world * self.K * self.n
             out = self.gathered[g * half:g * half + self.world * m * self.n]
         if self.timed:
-            rec = {"steps": m}
-            if hasattr(self.stream, "cuda_stream"):
-                rec["start"] = TimingEvent()
-                rec["start"].record(self.stream)
-            self.gather_rec.append(rec)
+            self.gather_rec.append({"steps": m})
         self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
         if self.timed and self.works[g] is not None:
             self._time_gather(self.works[g])
@@ -532,9 +526,9 @@ def rank_fields(kern_ms: list, gather_ms: list, el: float, steps: int, world: in
     """The N > 1 line's per-rank fields (collectives: every rank must call this).  el =
     this rank's wall seconds; returns (max over ranks of el, fields):
       per_rank_kernel_ms, kernel_ms_max_over_ranks — mean CRC launch time per rank;
-      per_rank_gather_ms, gather_ms_max_over_ranks — mean time per gather collective,
-        from its inputs being ready to its completion on the collective's stream
-        (Pipe._time_gather); gathers_per_rank = collectives in the timed region;
+      per_rank_gather_ms, gather_ms_max_over_ranks — mean duration of a gather collective
+        on its own stream (ProcessGroupNCCL's timing events, Pipe._time_gather);
+        gathers_per_rank = collectives timed in the timed region;
       step_ms — wall time per step (max over ranks);
       overlap — step_ms - kernel_ms_max_over_ranks: the step time the kernels do not
         explain.  About 0 when the gather hides behind the next CRC launches; about
@@ -678,6 +672,7 @@ def main():
         if world == 1:
             init_one_rank_group(local)
         else:
+            os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")  # the gathers' own durations (Pipe.gather_ms)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)

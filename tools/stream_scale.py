@@ -20,11 +20,13 @@ from bench import TimingEvent  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--out", default=None)
+ap.add_argument("--ns", default="1048576,2097152,4194304,8388608,15000000")
+ap.add_argument("--modes", default="pieces,stream")
 a = ap.parse_args()
 assert W.LIB.wtp_init(0) == 0
 st = torch.cuda.current_stream()
 rows = []
-for n in (1 << 20, 1 << 21, 1 << 22, 1 << 23, 15_000_000):
+for n in [int(x) for x in a.ns.split(",")]:
     lens = O.zipf_lengths(n, s=1.1)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.sum())
@@ -35,7 +37,8 @@ for n in (1 << 20, 1 << 21, 1 << 22, 1 << 23, 15_000_000):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     rb = total + 12 * n
     row = {"packets": n, "read_bytes": rb}
-    for mode in ("pieces", "stream"):
+    row["payload_bytes"] = total
+    for mode in a.modes.split(","):
         if mode == "stream":
             os.environ["WTP_STREAM_KERNEL"] = "1"
         f = lambda: W.crc32_batch_packed(d, total, do, dl, n, out)  # noqa: E731
