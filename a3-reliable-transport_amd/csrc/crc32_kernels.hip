@@ -1830,8 +1830,12 @@ __global__ __launch_bounds__(kStThreads) void k_stream(const uint8_t *__restrict
     uint32_t lA, lB, lC;
     load_group(lo, oA, lA);
     load_group(lo + 64, oB, lB);
-    const uint64_t o_lo = uniform64(__builtin_amdgcn_readfirstlane(uint32_t(oA)) |
-                                    (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(oA >> 32))) << 32));
+    // (uniform64 widens each half as unsigned: an earlier form OR'ed the int that
+    // readfirstlane returns into the 64-bit value, sign-extending the low half, so a wave
+    // whose first offset had bit 31 set got a garbage stream base and ran its whole range
+    // on the lane-per-payload path: exact, 6-7x slower, e.g. any wave starting between 2
+    // and 4 GiB into the buffer)
+    const uint64_t o_lo = uniform64(oA);
     const uint64_t wb = ((vabs + o_lo) & ~uint64_t(127)) - vabs;  // X0 (view offset, mod 2^64)
     uint64_t fb = hi;    // first payload that breaks the packing (wave-uniform)
     uint64_t pe = o_lo;  // end of the payload before the group being decoded
@@ -1978,6 +1982,7 @@ __global__ __launch_bounds__(kStThreads) void k_stream(const uint8_t *__restrict
     // --- payloads [fb, hi): one lane per payload, 16-B chunks straight from memory
     // (the next chunk prefetched while this one is fed word by word) --------------------
     typedef const __attribute__((address_space(1))) u32x4 gq;
+    if (fb < hi && lane == 0) atomicOr(status, 8u);  // informational: this batch left the fast path
     for (uint64_t g = fb; g < hi; g += 64) {
         const uint64_t p = g + lane, pc = p < hi ? p : hi - 1;
         const uint64_t o = off_of(pc);

@@ -82,9 +82,11 @@ int wtp_init(int device);
    that device from any thread. */
 int wtp_reserve_cus(int device, int ncus);
 
-/* Sticky device-side data-error flags of `device` (bit 0: a general-kernel payload
-   length was > WTP_MAX_KERNEL_LEN; that payload's result is then 0 / not ok).
-   Synchronous; clears the flags when `clear` != 0. */
+/* Sticky device-side flags of `device`.  Data errors: bit 0, a general-kernel payload
+   length was > WTP_MAX_KERNEL_LEN (that payload's result is then 0 / not ok); bit 2, see
+   wtp_crc32_verify_batch.  Informational: bit 3, the stream kernel met payloads that
+   were not packed (or >= 4096 B) and computed them on its slower per-payload path
+   (results exact).  Synchronous; clears the flags when `clear` != 0. */
 int wtp_device_status(int device, uint32_t *flags, int clear);
 
 /* ---- CPU reference semantics (single packet) --------------------------------------

@@ -607,7 +607,17 @@ def test_packed_breaks_and_edges(W, case):
     total = int((offs + lens).max()) + 16
     host = O.synth_fill_np(lead + total, start_byte=n)
     got = _run_packed(W, host, lead, offs, lens, total)
-    assert np.array_equal(got, O.batch_var(host[lead:], offs, lens)), case
+    want = O.batch_var(host[lead:], offs, lens)
+    assert np.array_equal(got, want), case
+    # the stream kernel on the same batch: exact, and its per-payload path (status bit 3)
+    # runs exactly when the batch breaks the packing or holds payloads >= 4096 B
+    W.device_status(0, clear=True)
+    out = u32_out(n)
+    _forced_stream(W)(dev_u8(host)[lead:], total, torch.from_numpy(offs.view(np.int64)).cuda(),
+                      torch.from_numpy(lens.view(np.int32)).cuda(), n, out)
+    assert np.array_equal(to_u32(out, n), want), case
+    slow = bool(W.device_status(0, clear=True) & 8)
+    assert slow == (case in ("gaps", "overlaps", "swapped", "long_4096")), case
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 127, 129, 511, 513, 4097])
@@ -633,6 +643,7 @@ def test_packed_view_over_4gib(W, VAR):
     n, L = 3_200_000, 1456
     total = n * L
     assert total > (1 << 32)
+    W.device_status(0, clear=True)
     d = torch.empty(total, dtype=torch.uint8, device="cuda")
     W.synth_fill(d)
     lens = np.full(n, L, np.uint32)
@@ -645,6 +656,9 @@ def test_packed_view_over_4gib(W, VAR):
     assert np.array_equal(got, to_u32(ref, n))
     for i in (0, 1, 2949840, 2949841, n - 1):  # payload 2949840 straddles 2^32, 2949841 starts past it
         assert int(got[i]) == O.crc32(O.synth_fill_np(L, start_byte=i * L)), i
+    # packed: every wave stays on the fast path, including waves starting between 2 and
+    # 4 GiB (a sign-extended wave base sent those to the per-payload path until round 5)
+    assert not (W.device_status(0, clear=True) & 8)
     del d
 
 
