@@ -847,7 +847,7 @@ struct RangeDesc {
 static_assert(sizeof(RangeDesc) == 32, "RangeDesc");
 // providers whose packet range and view are bound on the device (bind(), at kernel entry)
 template <class P>
-constexpr bool kDevRange = requires { P::kDevRange; };
+constexpr bool kDevRange = requires { requires P::kDevRange; };  // declared and true
 struct CrcEpi {
     static constexpr const char *kName = "CrcEpi";  // wtp_last_kernel()
     uint32_t *out;
