@@ -91,6 +91,35 @@ def test_long_batch_into_unaligned_out(W):
         assert (guard[:shift] == 0x5A5A5A5A).all() and (guard[shift + n:] == 0x5A5A5A5A).all(), shift
 
 
+def test_last_kernel_names_every_route(W):
+    """wtp_last_kernel() (bench.py's roofline.kernel) names the instantiation each route
+    launched: braided direct / held, the general kernel for odd shapes and mixed lengths,
+    the stream kernel when forced, the verify and builder epilogues."""
+    name = lambda: W.LIB.wtp_last_kernel().decode()  # noqa: E731
+    buf = torch.empty(4096 * 1472 + 64, dtype=torch.uint8, device="cuda")
+    W.synth_fill(buf)
+    out = u32_out(4096)
+    W.crc32_batch_fixed(buf, 1456, 1456, 4096, out)
+    assert name() == "k_fixed_braid<6, 0, CrcBEpi>"
+    W.crc32_batch_fixed(buf, 1457, 1000, 3000, out)
+    assert name() == "k_pieces<FixedProvL, CrcEpi>"
+    offs = torch.arange(0, 4096 * 100, 100, dtype=torch.int64, device="cuda")
+    lens = torch.full((4096,), 100, dtype=torch.int32, device="cuda")
+    W.crc32_batch_var(buf, 4096 * 1472, offs, lens, 4096, out)
+    assert name() == "k_pieces<ArrayProvL, CrcEpi>"
+    _forced_stream(W)(buf, 4096 * 1472, offs, lens, 4096, out)
+    assert name() == "k_stream"
+    wire = torch.empty(4096 * 1472 + 64, dtype=torch.uint8, device="cuda")
+    wl = torch.empty(4096, dtype=torch.int32, device="cuda")
+    W.build_data_packets(buf, 4096 * 1456, 0, wire, 1472, wl)
+    assert name() == "k_fixed_braid<6, 0, BuildBEpi>"
+    ok = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    W.verify_batch(wire, 1472, wl, 4096, ok)
+    assert name() == "k_fixed_braid<6, 0, VerifyBEpi>"
+    torch.cuda.synchronize()
+    assert bool(ok.all())
+
+
 def test_fixed_held_results_past_2g_result_bytes(W):
     """Held results (CrcHoldBEpi, long batches) past 2^29 packets: 16-B payloads, n =
     2^29 + 1237 (8.6 GB of payloads, 2.1 GB of results), so result byte offsets pass 2^31
