@@ -66,6 +66,9 @@ def parse():
                     help="with the gather: gather the results of this many steps in one collective (the step's "
                          "stream-event hops are paid once per group; 2: 0.480 -> 0.468 ms per C4 step, "
                          "profiles/r04e)")
+    ap.add_argument("--result-groups", type=int, default=2,
+                    help="with the gather: result-slot groups in rotation (a group is rewritten only after its "
+                         "previous gather is done; more groups push that wait further behind)")
     ap.add_argument("--gather-n1", action="store_true",
                     help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box streaming-read probe")
@@ -377,18 +380,19 @@ class Pipe:
     """Step i: the CRC of this rank's shard into a result slot on `stream`, then (with the
     gather) the RCCL gather of the results to rank 0, asynchronous: it runs on the
     collective's stream, on the CUs the CRC kernel leaves free (wtp_reserve_cus), while
-    the next steps' CRCs run.  Result slots come in two groups of `every` slots; a group is
+    the next steps' CRCs run.  Result slots come in `groups` groups (default 2) of `every` slots; a group is
     gathered in one collective when it is full (every = 1: each step's results right
     after its launch), and rewritten only after that gather is done.  `bufs` may hold
     several shards of equal size: step i reads bufs[i % len(bufs)] (the alternating-buffer
     leg).  `gathered` (rank 0) holds 2 x world x every x n results: one half per group."""
 
-    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1):
+    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1, groups=2):
         import torch
         self.W, self.shard, self.bufs, self.n, self.stream = W, shard, bufs, n, stream
         self.do_gather, self.world, self.rank, self.gathered = do_gather, world, rank, gathered
         self.K = max(1, int(every)) if do_gather else 1
-        self.groups = [torch.empty(self.K * n, dtype=torch.int32, device=dev) for _ in range(2 if do_gather else 1)]
+        ng = max(2, int(groups)) if do_gather else 1
+        self.groups = [torch.empty(self.K * n, dtype=torch.int32, device=dev) for _ in range(ng)]
         self.works = [None] * len(self.groups)
         self.i = 0       # steps launched
         self.pos = 0     # result slots used (a flush skips to the next group)
@@ -564,7 +568,8 @@ def kstats(kern: list, nbytes: int) -> dict:
             "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4_PACKETS // 8, every: int = 1) -> dict:
+def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4_PACKETS // 8, every: int = 1,
+                 groups: int = 2) -> dict:
     """Equal-work reference for the N > 1 lines, in the N = 1 process: rank 0's C4 shard
     (2 M x 1456 B = 3.05 GB, the first 2 M packets of the global stream) through the SAME
     pipelined step the N > 1 ranks run (own stream, 8 reserved CUs, the asynchronous RCCL
@@ -586,8 +591,8 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
     torch.cuda.set_stream(stream)
     W.reserve_cus(8, torch.cuda.current_device())
     try:
-        gathered = torch.empty(2 * every * n, dtype=torch.int32, device=dev)
-        pipe = Pipe(W, shard, [buf], n, stream, True, 1, 0, gathered, dev, every=every)
+        gathered = torch.empty(max(2, groups) * every * n, dtype=torch.int32, device=dev)
+        pipe = Pipe(W, shard, [buf], n, stream, True, 1, 0, gathered, dev, every=every, groups=groups)
         settle(pipe.step, stream, warmup)
         pipe.drain()
         torch.cuda.synchronize()
@@ -648,7 +653,8 @@ def run_extra_legs(line: dict, parity: dict, W, shard, buf, nbytes: int, n: int,
     except (RuntimeError, OSError) as e:  # WtpError is a RuntimeError
         line["alt_buffer"] = {"error": f"{e.__class__.__name__}: {e}"[:300]}
     try:
-        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup, every=args.gather_every)
+        line["c4_shard_1gpu"] = c4_shard_leg(W, shard, dev, local, args.steps, args.warmup, every=args.gather_every,
+                                             groups=getattr(args, "result_groups", 2))
         if line["c4_shard_1gpu"]["parity_match"] is False:
             parity["c4_shard_1gpu"] = False
     except (RuntimeError, OSError) as e:
@@ -699,8 +705,9 @@ def main():
     if reserve:
         W.reserve_cus(reserve, torch.cuda.current_device())
     every = args.gather_every if do_gather else 1
-    gathered = torch.empty(2 * world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
-    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every)
+    ngroups = max(2, args.result_groups) if do_gather else 1
+    gathered = torch.empty(ngroups * world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
+    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every, groups=ngroups)
     out = torch.empty(n, dtype=torch.int32, device=dev)  # the read-probe leg's CRC launches
 
     def crc():
@@ -757,6 +764,7 @@ def main():
                    "parallelism": f"packet shards x{world}" if world > 1 else "single GPU",
                    "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
                    "gather_every": every if do_gather else None,
+                   "result_groups": ngroups if do_gather else None,
                    "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,

@@ -225,7 +225,7 @@ def test_gather_async_requires_out_on_dst():
         shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=torch.zeros(7, dtype=torch.int32))
 
 
-def _bench_pipe_worker(rank, world, port, every, steps, q):
+def _bench_pipe_worker(rank, world, port, every, steps, q, groups=2):
     """bench.py's own Pipe (results gathered in groups of `every` steps, two groups in
     flight, a partial group flushed at the end) over gloo, with a stand-in launch that
     writes rank * 1000 + step * 7 + lane into the step's result slot."""
@@ -248,8 +248,8 @@ def _bench_pipe_worker(rank, world, port, every, steps, q):
             out.copy_(torch.arange(nn, dtype=torch.int32) + rank * 1000 + FakeW.calls * 7)
             FakeW.calls += 1
 
-    gathered = torch.empty(2 * world * every * n, dtype=torch.int32) if rank == 0 else None
-    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every)
+    gathered = torch.empty(groups * world * every * n, dtype=torch.int32) if rank == 0 else None
+    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every, groups=groups)
     seen = []
     real = S.gather_crcs_async
 
@@ -267,13 +267,15 @@ def _bench_pipe_worker(rank, world, port, every, steps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,every,steps", [(2, 1, 3), (2, 2, 5), (3, 4, 6), (8, 2, 5)])
-def test_bench_pipe_grouped_gather(world, every, steps):
+@pytest.mark.parametrize("world,every,steps,groups", [(2, 1, 3, 2), (2, 2, 5, 2), (3, 4, 6, 2), (8, 2, 5, 2),
+                                                      (2, 2, 9, 3), (3, 1, 7, 8)])
+def test_bench_pipe_grouped_gather(world, every, steps, groups):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_pipe_worker, args=(r, world, port, every, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bench_pipe_worker, args=(r, world, port, every, steps, q, groups))
+             for r in range(world)]
     for p in procs:
         p.start()
     got, seen = q.get(timeout=180)
