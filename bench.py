@@ -14,11 +14,14 @@ runs config C4's per-GPU shard, 2 M x 1456 B per rank, so that N = 8 is exactly 
 `--gpus N` (N > 1) without torchrun starts N rank processes itself (one per GPU).
 
 Rank 0 prints ONE JSON line.  value = GiB/s of payload over all ranks (whole job, max
-time over ranks); roofline = the CRC kernel's algorithmic read bytes per launch / its
-mean HIP-event duration vs the 8 TB/s HBM peak, next to the same box's streaming-read
-probe (a plain nt read kernel timed in the same process: a reference point, not a bound); roofline.traffic = the PMC
-pass's HBM bytes, reported only while the shipped kernel's code hash matches the one
-measured; kernel_us = every timed launch; parity = sha256 of the whole result vector vs
+time over ranks); the timed region holds nothing between the launches but the work, one
+HIP event pair on the CRC stream around it; roofline = the CRC kernel's algorithmic read
+bytes per launch / (that region's event time / K) vs the 8 TB/s HBM peak, next to the same
+box's streaming-read probe (a plain nt read kernel timed in the same process: a reference
+point, not a bound); roofline.traffic = the PMC pass's HBM bytes, reported only while the
+shipped kernel's code hash matches the one measured; roofline.instrumented_pass and
+kernel_us_instrumented_pass = the same K steps run again with an event pair around every
+launch (untimed: those events cost ~5 us per step); parity = sha256 of the whole result vector vs
 the reference's digest; cpu_baseline = the reference's own crc32 (oracle/_ref, compiled
 from cpp/src/common/Crc32.hpp) timed on this host's cores over a bounded sample.
 N = 1 adds two legs after the timed region (--no-extras skips them): alt_buffer (the
@@ -497,33 +500,43 @@ class Pipe:
         return g.view(self.world, m * self.n)[:, (m - 1) * self.n:].reshape(-1)
 
 
-def time_steps(pipe: Pipe, steps: int, world: int):
-    """Exactly `steps` timed steps, barrier + synchronize on both sides; the start/end HIP
-    events bracket each CRC launch on its stream (the gather runs on the collective's
-    stream).  Returns (kernel ms per launch, wall seconds, this rank only)."""
+def time_steps(pipe: Pipe, steps: int, world: int, per_launch: bool = False):
+    """Exactly `steps` steps, barrier + synchronize on both sides.  One HIP event pair on
+    the CRC stream brackets the whole run (the gather runs on the collective's stream).
+    per_launch=False is the timed region: nothing between the launches but the work (an
+    event pair around every launch cost ~5 us per 215 us step, 2.5%: profiles/r05v).
+    per_launch=True adds that pair around every launch: the instrumented pass that gives
+    the per-launch kernel times.  Returns (per-launch kernel ms or None, ms between the
+    two region events, wall seconds; this rank only)."""
     import torch
     import torch.distributed as dist
 
-    starts = [TimingEvent() for _ in range(steps)]
-    ends = [TimingEvent() for _ in range(steps)]
+    starts = [TimingEvent() for _ in range(steps)] if per_launch else None
+    ends = [TimingEvent() for _ in range(steps)] if per_launch else None
+    r0, r1 = TimingEvent(), TimingEvent()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     pipe.gather_rec, pipe.timed = [], True  # the gathers of these steps are timed (Pipe.gather_ms)
     t0 = time.perf_counter()
+    r0.record(pipe.stream)
     for i in range(steps):
         pipe.wait_slot()  # (stream-side) before the start event: it times the kernel alone
-        starts[i].record(pipe.stream)
+        if per_launch:
+            starts[i].record(pipe.stream)
         pipe.launch()
-        ends[i].record(pipe.stream)
+        if per_launch:
+            ends[i].record(pipe.stream)
         pipe.finish()
+    r1.record(pipe.stream)
     pipe.drain()  # gathers a partly filled group, waits for every gather
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     pipe.timed = False
-    return [s.elapsed_time(e) for s, e in zip(starts, ends)], el
+    kern = [s.elapsed_time(e) for s, e in zip(starts, ends)] if per_launch else None
+    return kern, r0.elapsed_time(r1), el
 
 
 def rank_fields(kern_ms: list, gather_ms: list, el: float, steps: int, world: int, dev) -> tuple[float, dict]:
@@ -596,8 +609,9 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
         settle(pipe.step, stream, warmup)
         pipe.drain()
         torch.cuda.synchronize()
-        kern, el = time_steps(pipe, steps, 1)
+        _, region_ms, el = time_steps(pipe, steps, 1)  # timed: step_ms, value_GiBs
         gms = pipe.gather_ms()
+        kern, _, _ = time_steps(pipe, steps, 1, per_launch=True)  # instrumented: kernel time
         import numpy as np
         par = parity_digest(pipe.gathered_vector().cpu().numpy().view(np.uint32))
     finally:
@@ -610,7 +624,10 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
            "packets": n, "bytes_per_launch": nbytes, "steps": steps,
            "gather_every": pipe.K,
            "step_ms": round(el / steps * 1e3, 4), "value_GiBs": round(nbytes * steps / el / 2**30, 2),
-           "parity_match": par["match"], "sha256": par["sha256"]}
+           "region_ms_per_step": round(region_ms / steps, 5),
+           "parity_match": par["match"], "sha256": par["sha256"],
+           "timing": "step_ms / value_GiBs: a timed pass with no events between launches; kernel_ms_*: a "
+                     "second pass of as many steps with an event pair around every launch"}
     out.update(kstats(kern, nbytes))
     out["gather_ms"] = round(sum(gms) / len(gms), 5) if gms else None
     out["gathers"] = len(gms)
@@ -633,10 +650,15 @@ def alt_buffer_leg(W, buf, nbytes: int, n: int, dev, stream, steps: int, warmup:
     torch.cuda.synchronize()
     if pipe.i % 2:
         pipe.step()
-    kern, el = time_steps(pipe, steps, 1)
+    _, region_ms, el = time_steps(pipe, steps, 1)
+    if pipe.i % 2:
+        pipe.step()
+    kern, _, _ = time_steps(pipe, steps, 1, per_launch=True)
     out = {"what": "k_fixed_braid<6> alternating between two 1 M x 1456 B buffers (the next 1 M packets "
                    "of the stream), current stream, no gather",
-           "steps": steps, "step_ms": round(el / steps * 1e3, 4)}
+           "steps": steps, "step_ms": round(el / steps * 1e3, 4), "region_ms_per_step": round(region_ms / steps, 5),
+           "timing": "step_ms: a timed pass with no events between launches; kernel_ms_*: a second pass with an "
+                     "event pair around every launch"}
     out.update(kstats(kern, nbytes))
     out["alt_buffer_kernel_ms"] = out["kernel_ms_mean"]
     del buf2
@@ -717,14 +739,20 @@ def main():
     pipe.drain()
     torch.cuda.synchronize()
 
-    kern, el = time_steps(pipe, args.steps, world)
+    # the timed region: exactly K steps, nothing between the launches but the work
+    _, region_ms, el = time_steps(pipe, args.steps, world)
     kernel_name = W.LIB.wtp_last_kernel().decode()  # the instantiation the timed launches used
+    gms = pipe.gather_ms()
+    kmean = region_ms / args.steps  # average launch duration over the timed region (its two events)
+    # then as many steps again with an event pair around every launch (untimed diagnostics:
+    # the per-launch distribution, and the kernel time the N > 1 `overlap` is read against)
+    kern, _, _ = time_steps(pipe, args.steps, world, per_launch=True)
     kern_ms = sorted(kern)
-    kmean = sum(kern_ms) / len(kern_ms)
+    kmean_pl = sum(kern_ms) / len(kern_ms)
 
     per_rank = None
     if world > 1 or args.gather_n1:  # --gather-n1: the same fields from a one-rank RCCL world
-        el, per_rank = rank_fields(kern, pipe.gather_ms(), el, args.steps, world, dev)
+        el, per_rank = rank_fields(kern, gms, el, args.steps, world, dev)
 
     # parity of the WHOLE result vector (rank 0: the gathered vector when N > 1)
     parity = None
@@ -769,12 +797,16 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,
                      "kernel": kernel_name, "kernel_ms_mean": round(kmean, 5),
-                     "kernel_ms_median": round(kern_ms[len(kern_ms) // 2], 5),
-                     "kernel_ms_p10": round(kern_ms[len(kern_ms) // 10], 5),
-                     "kernel_ms_p90": round(kern_ms[(9 * len(kern_ms)) // 10], 5),
+                     "kernel_ms_rule": "HIP events on the CRC stream around the timed region's K launches, / K",
+                     "instrumented_pass": {"what": "the same K steps again, an event pair around every launch "
+                                                   "(not part of value: ~5 us per step, profiles/r05v)",
+                                           "kernel_ms_mean": round(kmean_pl, 5),
+                                           "kernel_ms_median": round(kern_ms[len(kern_ms) // 2], 5),
+                                           "kernel_ms_p10": round(kern_ms[len(kern_ms) // 10], 5),
+                                           "kernel_ms_p90": round(kern_ms[(9 * len(kern_ms)) // 10], 5)},
                      "bytes_per_launch": nbytes,
                      "frac_of_same_box_read_probe": round(achieved / probe["GBs"], 4) if probe else None},
-        "kernel_us": [round(k * 1e3, 1) for k in kern],
+        "kernel_us_instrumented_pass": [round(k * 1e3, 1) for k in kern],
         "warmup_run": warm_done,
         "warmup_rule": "max(--warmup, 100) launches, then until 3 consecutive 25-launch block means agree "
                        "within 1% (cap 3 s); untimed",

@@ -167,7 +167,7 @@ def test_n1_extra_legs_fields_on_cpu(monkeypatch, every):
     assert c4["packets"] == n and c4["bytes_per_launch"] == nbytes and c4["steps"] == 4
     assert c4["gather_every"] == every  # every = 3 over 4 steps: one full group, one partial
     assert W.reserved == [8, 0]  # 8 CUs for the gather while the leg runs, then restored
-    assert W.launches == 3 + 4  # settle + the timed steps, one launch each
+    assert W.launches == 3 + 4 + 4  # settle, the timed steps, the instrumented pass: one launch each
     want = O.batch_fixed(O.synth_fill_np(nbytes), bench.PAYLOAD, bench.PAYLOAD, n)
     assert c4["sha256"] == hashlib.sha256(want.astype("<u4").tobytes()).hexdigest()[:16]
     assert c4["parity_match"] is None  # no reference digest at this size; the real leg has one

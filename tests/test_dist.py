@@ -326,8 +326,11 @@ def _rank_fields_worker(rank, world, port, every, steps, q):
     for _ in range(3):  # untimed warmup: its gathers are not counted
         pipe.step()
     pipe.drain()
-    kern, el = bench.time_steps(pipe, steps, world)
-    el_max, f = bench.rank_fields(kern, pipe.gather_ms(), el, steps, world, "cpu")
+    _, region, el = bench.time_steps(pipe, steps, world)  # the timed pass
+    gms = pipe.gather_ms()
+    kern, _, _ = bench.time_steps(pipe, steps, world, per_launch=True)  # the instrumented pass
+    assert kern is not None and len(kern) == steps and region > 0
+    el_max, f = bench.rank_fields(kern, gms, el, steps, world, "cpu")
     if rank == 0:
         q.put((f, el_max, el))
     dist.barrier()
