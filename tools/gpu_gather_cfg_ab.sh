@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="gpurun_out/${1:-gcfg}"; mkdir -p "$OUT"
 for rep in 1 2 3; do
-  for cfg in "2 2" "2 8" "4 4" "1 8"; do
+  for cfg in ${CFGS:-"2 2" "2 8" "4 4" "1 8"}; do
     set -- $cfg
     timeout -k 10 200 python bench.py --gather-n1 --packets-per-rank 2097152 --steps 40 --warmup 5 --no-cpu-baseline --no-probe \
       --gather-every $1 --result-groups $2 > "$OUT/e$1_g$2_r$rep.log" 2>&1 || exit $?
