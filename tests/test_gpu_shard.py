@@ -156,7 +156,8 @@ def test_bench_pipelined_gather_one_rank(W):
     assert line["parity"]["match"] is True, line["parity"]
     # the N > 1 line's per-rank fields, here from RCCL collectives in a one-rank world
     assert line["per_rank_kernel_ms"] == [line["kernel_ms_max_over_ranks"]] and line["kernel_ms_max_over_ranks"] > 0
-    assert line["gathers_per_rank"] == [3] and line["per_rank_gather_ms"][0] > 0  # 5 steps, pairs: 2 + flushed 1
+    every = line["config"]["gather_every"]
+    assert line["gathers_per_rank"] == [-(-5 // every)] and line["per_rank_gather_ms"][0] > 0  # full groups + the flushed one
     assert abs(line["overlap"] - (line["step_ms"] - line["kernel_ms_max_over_ranks"])) < 1e-4
 
 
