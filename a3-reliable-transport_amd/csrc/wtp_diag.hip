@@ -98,6 +98,13 @@ int wtp_diag_event_elapsed_ms(void *start, void *end, float *ms) {
     return hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(end)) == hipSuccess ? 0 : -2;
 }
 
+// Make `stream` wait for `ev` (a timing-only event): a cross-stream dependency whose
+// record on the producer stream carries no system-scope fence (bench.py --gather-helper).
+int wtp_diag_stream_wait(void *stream, void *ev) {
+    if (!ev) return -1;
+    return hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(ev), 0) == hipSuccess ? 0 : -2;
+}
+
 int wtp_diag_event_destroy(void *ev) {
     if (!ev) return 0;
     return hipEventDestroy(static_cast<hipEvent_t>(ev)) == hipSuccess ? 0 : -2;

@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--result-groups", type=int, default=2,
                     help="with the gather: result-slot groups in rotation (a group is rewritten only after its "
                          "previous gather is done; more groups push that wait further behind)")
+    ap.add_argument("--gather-helper", action="store_true",
+                    help="A/B: issue the gathers from a helper stream joined to the CRC stream by fence-free events")
     ap.add_argument("--gather-n1", action="store_true",
                     help="N=1: run the pipelined RCCL gather in a one-rank world (exercises the N>1 step on one GPU)")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box streaming-read probe")
@@ -273,6 +275,7 @@ def diag():
         D.wtp_diag_event_record.argtypes = [C.c_void_p, C.c_void_p]
         D.wtp_diag_event_elapsed_ms.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]
         D.wtp_diag_event_destroy.argtypes = [C.c_void_p]
+        D.wtp_diag_stream_wait.argtypes = [C.c_void_p, C.c_void_p]
         _DIAG = D
     return _DIAG
 
@@ -389,7 +392,8 @@ class Pipe:
     several shards of equal size: step i reads bufs[i % len(bufs)] (the alternating-buffer
     leg).  `gathered` (rank 0) holds 2 x world x every x n results: one half per group."""
 
-    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1, groups=2):
+    def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1, groups=2,
+                 helper=False):
         import torch
         self.W, self.shard, self.bufs, self.n, self.stream = W, shard, bufs, n, stream
         self.do_gather, self.world, self.rank, self.gathered = do_gather, world, rank, gathered
@@ -403,6 +407,21 @@ class Pipe:
         self.last_pos = 0
         self.timed = False  # time_steps sets it: the gathers issued meanwhile are timed
         self.gather_rec = []
+        # --gather-helper (A/B option): the collectives are issued from a helper stream that
+        # meets the CRC stream only through fence-free events, so torch's own cross-stream
+        # events are recorded on the helper, not between the CRC launches
+        self.helper = None
+        if helper and do_gather and hasattr(stream, "cuda_stream"):
+            self.helper = torch.cuda.Stream()
+        self._keep = []  # events of the current step pair (alive until their waits are queued)
+
+    def _hop(self, src, dst):
+        """dst waits for everything queued on src so far (a fence-free event)."""
+        ev = TimingEvent()
+        ev.record(src)
+        if diag().wtp_diag_stream_wait(dst.cuda_stream, ev.e) != 0:
+            raise RuntimeError("wtp_diag_stream_wait failed")
+        self._keep.append(ev)
 
     def _time_gather(self, work):
         """Record one gather for gather_ms().  RCCL: the collective's own duration on its
@@ -439,7 +458,13 @@ class Pipe:
         if self.pos % self.K == 0:  # first slot of a group: its previous gather must be done
             g = self._group(self.pos)
             if self.works[g] is not None:
-                self.works[g].wait()
+                if self.helper is not None:
+                    import torch
+                    with torch.cuda.stream(self.helper):
+                        self.works[g].wait()
+                    self._hop(self.helper, self.stream)
+                else:
+                    self.works[g].wait()
                 self.works[g] = None
 
     def launch(self):
@@ -458,7 +483,16 @@ class Pipe:
             out = self.gathered[g * half:g * half + self.world * m * self.n]
         if self.timed:
             self.gather_rec.append({"steps": m})
-        self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
+        if self.helper is not None:
+            import torch
+            self._hop(self.stream, self.helper)
+            with torch.cuda.stream(self.helper):
+                self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank,
+                                                             out=out)
+            if len(self._keep) > 64:
+                self._keep = self._keep[-8:]
+        else:
+            self.works[g] = self.shard.gather_crcs_async(self.groups[g][:m * self.n], self.world, self.rank, out=out)
         if self.timed and self.works[g] is not None:
             self._time_gather(self.works[g])
         self.last_m, self.last_g = m, g
@@ -485,7 +519,13 @@ class Pipe:
         self.flush()
         for b, w in enumerate(self.works):
             if w is not None:
-                w.wait()
+                if self.helper is not None:
+                    import torch
+                    with torch.cuda.stream(self.helper):
+                        w.wait()
+                    self._hop(self.helper, self.stream)
+                else:
+                    w.wait()
                 self.works[b] = None
 
     def last_out(self):
@@ -729,7 +769,8 @@ def main():
     every = args.gather_every if do_gather else 1
     ngroups = max(2, args.result_groups) if do_gather else 1
     gathered = torch.empty(ngroups * world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
-    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every, groups=ngroups)
+    pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every, groups=ngroups,
+                helper=args.gather_helper)
     out = torch.empty(n, dtype=torch.int32, device=dev)  # the read-probe leg's CRC launches
 
     def crc():
@@ -793,6 +834,7 @@ def main():
                    "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
                    "gather_every": every if do_gather else None,
                    "result_groups": ngroups if do_gather else None,
+                   "gather_helper_stream": bool(args.gather_helper) if do_gather else None,
                    "reserved_cus": reserve},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,

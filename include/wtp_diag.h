@@ -32,6 +32,8 @@ int wtp_diag_event_create(void **ev);
 int wtp_diag_event_record(void *ev, void *stream);
 int wtp_diag_event_elapsed_ms(void *start, void *end, float *ms);
 int wtp_diag_event_destroy(void *ev);
+/* `stream` waits for event `ev` (hipStreamWaitEvent). */
+int wtp_diag_stream_wait(void *stream, void *ev);
 
 #ifdef __cplusplus
 }
