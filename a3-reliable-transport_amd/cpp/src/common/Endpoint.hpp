@@ -11,6 +11,7 @@
 #include <sys/time.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -142,7 +143,8 @@ class Checksums {
         char *end = nullptr;
         errno = 0;
         const unsigned long long v = std::strtoull(e, &end, 10);
-        if (errno != 0 || end == e || *end != '\0' || *e == '-' || *e == '+' || *e == ' ')
+        // the first character must be a digit: strtoull skips any leading whitespace and sign
+        if (errno != 0 || end == e || *end != '\0' || !std::isdigit(static_cast<unsigned char>(*e)))
             throw std::invalid_argument(std::string("WTP_VERIFY_CPU_MAX_BYTES: not a decimal byte count: '") + e + "'");
         return size_t(v);
     }

@@ -837,9 +837,12 @@ struct MetaRaw {
 };
 // One sub-launch of a packed batch >= 2 GiB (launch_packed_ranges): packets [begin, end)
 // of the caller's arrays, read through a < 2 GiB view that starts `rebase` bytes into the
-// 16-B aligned buffer.  Written on the device by k_cut_ranges; `bad` is set by the piece
-// kernel when a packet lies outside the view (the offsets were not packed), and then a
-// gated k_stream launch recomputes the whole batch.
+// 16-B aligned buffer.  Written on the device by k_cut_ranges.  `bad` holds two flags:
+// kCutBad, set by k_cut_ranges (an offset past the buffer; fixed before any piece
+// sub-launch starts, so every wave of a sub-launch reads the same value), and kRunBad, set
+// by the piece kernel when a packet lies outside the view (the offsets were not packed).
+// Either one makes the gated k_stream launch recompute the whole batch.
+constexpr uint32_t kRunBad = 1u, kCutBad = 2u;
 struct RangeDesc {
     uint64_t begin, end, rebase;
     uint32_t nbytes, bad;
@@ -2126,6 +2129,8 @@ int fail(int code, const char *fmt, ...) {
         if (e_ != hipSuccess) return fail(WTP_EHIP, "%s: %s", #call, hipGetErrorString(e_)); \
     } while (0)
 
+constexpr size_t kStreamScratch = 32768;  // launch_packed_ranges' descriptors (one call)
+constexpr unsigned kCaptureSlots = 64;     // descriptor buffers for calls captured into graphs
 struct DevState {
     std::once_flag once;
     int rc = WTP_OK;
@@ -2136,13 +2141,20 @@ struct DevState {
     std::atomic<int> reserve{0};  // CUs left free of the persistent kernels (wtp_reserve_cus)
     unsigned grid_cus() const { return unsigned(std::max(1, cus - reserve.load(std::memory_order_relaxed))); }
     hipMemPool_t pool = nullptr;  // library-owned stream-ordered pool, never trimmed (builder scratch)
-    // Per-stream device scratch of fixed size (launch_packed_ranges' descriptors): made on
-    // a stream's first use outside graph capture and kept, so calls captured into a graph
-    // bake in a buffer that outlives the graph.  (Stream-ordered pool allocations inside a
+    // Device scratch of fixed size for launch_packed_ranges' descriptors.  Outside graph
+    // capture: one buffer per stream, made on the stream's first use and kept (calls on one
+    // stream are ordered, so they may share it).  During capture: a slot of `cap`, taken
+    // by that one captured call for the life of the process, so two graphs captured on one
+    // stream (torch's shared capture stream) never share descriptors when replayed at
+    // once; with every slot taken, a captured call takes k_stream instead (exact, no
+    // scratch).  Both kinds are plain hipMalloc memory made outside any capture, so a graph
+    // bakes in a buffer that outlives it.  (Stream-ordered pool allocations inside a
     // capture replayed wrongly when one graph held several calls: the sub-launches read
     // zeroed descriptors and did nothing; profiles/r05)
     std::mutex smu;
     std::unordered_map<hipStream_t, void *> sbuf;
+    uint8_t *cap = nullptr;  // kCaptureSlots x kStreamScratch, made at init
+    unsigned cap_used = 0;
 };
 constexpr int kMaxDev = 64;
 DevState g_dev[kMaxDev];
@@ -2202,6 +2214,8 @@ int init_device(int dev) {
             pp.allocType = hipMemAllocationTypePinned;
             pp.location.type = hipMemLocationTypeDevice;
             pp.location.id = dev;
+            if (hipMalloc(&s.cap, kCaptureSlots * kStreamScratch) != hipSuccess)
+                return setfail(WTP_ENOMEM, "hipMalloc(capture scratch) failed");
             if (hipMemPoolCreate(&s.pool, &pp) != hipSuccess) return setfail(WTP_EHIP, "hipMemPoolCreate failed");
             uint64_t keep = UINT64_MAX;
             if (hipMemPoolSetAttribute(s.pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
@@ -2224,20 +2238,22 @@ int current(DevState *&s) {
     return WTP_OK;
 }
 
-// The stream's scratch buffer (kStreamScratch bytes), made on first use.  A first use
-// while the stream is capturing a graph is an error (no allocation may happen there).
-constexpr size_t kStreamScratch = 32768;
+// Descriptor scratch (kStreamScratch bytes) for one launch_packed_ranges call on `st`
+// (DevState::sbuf / cap).  *out = nullptr: the call is being captured and every capture
+// slot is taken; the caller then takes the scratch-free k_stream route.
 int stream_scratch(DevState &s, hipStream_t st, void **out) {
     std::lock_guard<std::mutex> g(s.smu);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    WTP_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+        *out = s.cap_used < kCaptureSlots ? s.cap + kStreamScratch * s.cap_used++ : nullptr;
+        return WTP_OK;
+    }
     auto it = s.sbuf.find(st);
     if (it != s.sbuf.end()) {
         *out = it->second;
         return WTP_OK;
     }
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    WTP_HIP(hipStreamIsCapturing(st, &cs));
-    if (cs != hipStreamCaptureStatusNone)
-        return fail(WTP_EINVAL, "packed batch >= 2 GiB: the stream's first such call must run outside graph capture");
     void *p = nullptr;
     WTP_HIP(hipMalloc(&p, kStreamScratch));
     s.sbuf.emplace(st, p);
@@ -2438,7 +2454,9 @@ struct RangeArrayProvL {
     template <class E>
     __device__ __forceinline__ bool bind(const uint8_t *&base, uint32_t &nbytes, uint64_t &nn, E &e) {
         const uint64_t b = desc->begin, en = desc->end;
-        if (b >= en || desc->bad) return false;
+        // only the cut-time flag: kRunBad may be set by another workgroup mid-launch, and
+        // reading it here could let some waves of a block leave before a barrier
+        if (b >= en || (desc->bad & kCutBad)) return false;
         rebase = desc->rebase;
         vbytes = desc->nbytes;
         offs += b;
@@ -2450,7 +2468,7 @@ struct RangeArrayProvL {
         e.rebase(b, n);
         return true;
     }
-    __device__ __forceinline__ void flag_outside() const { atomicOr(&desc->bad, 1u); }
+    __device__ __forceinline__ void flag_outside() const { atomicOr(&desc->bad, kRunBad); }
     __device__ __forceinline__ void load(uint64_t p, MetaRaw &r, __amdgpu_buffer_rsrc_t) const {
         r.a = offs[p];
         r.b = lens[p];
@@ -2530,7 +2548,7 @@ __global__ __launch_bounds__(256) void k_cut_ranges(const uint64_t *__restrict__
                 d.rebase = r;
                 d.nbytes = uint32_t(vspan - r < (1ull << 31) - 16 ? vspan - r : (1ull << 31) - 16);
             } else {
-                d.bad = 1;  // an offset past the buffer: not a packed batch
+                d.bad = kCutBad;  // an offset past the buffer: not a packed batch
             }
         }
         desc[j] = d;
@@ -2596,6 +2614,7 @@ int launch_packed_ranges(DevState &s, const uint8_t *b, uint64_t base_bytes, con
     dev::RangeDesc *d = nullptr;
     int rc = stream_scratch(s, st, reinterpret_cast<void **>(&d));
     if (rc) return rc;
+    if (!d) return launch_stream(s, b, base_bytes, offs, lens, n, out, st);  // captured, no slot left
     hipLaunchKernelGGL(dev::k_cut_ranges, dim3(1), dim3(256), 0, st, offs, n, lead, vspan, G, uint32_t(kb),
                        uint64_t(kSubBatch), d, uint32_t(nd));
     rc = launch_check("k_cut_ranges");

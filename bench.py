@@ -24,11 +24,16 @@ kernel_us_instrumented_pass = the same K steps run again with an event pair arou
 launch (untimed: those events cost ~5 us per step); parity = sha256 of the whole result vector vs
 the reference's digest; cpu_baseline = the reference's own crc32 (oracle/_ref, compiled
 from cpp/src/common/Crc32.hpp) timed on this host's cores over a bounded sample.
-N = 1 adds two legs after the timed region (--no-extras skips them): alt_buffer (the
-kernel alternating between two 1 M buffers, as a streaming sender would) and
+N = 1 adds legs after the timed region (--no-extras skips them): alt_buffer (the
+kernel alternating between two 1 M buffers, as a streaming sender would),
 c4_shard_1gpu (rank 0's 2 M-packet C4 shard through the N > 1 pipelined step with a
-one-rank RCCL gather: the equal-work reference for the N > 1 lines).  N > 1 lines add
-per-rank kernel and gather times, step_ms and overlap (rank_fields).
+one-rank RCCL gather: the equal-work reference for the N > 1 lines) and configs (every
+other BASELINE config: C2, C3, C5 Zipf 1.1 / 1.0, receiver verify, the builders; each row
+with back-to-back and graph times, its roofline fraction and parity of its whole result
+against a reference-computed digest; tools/config_legs.py, --no-configs skips it).  N > 1
+lines add per-rank kernel, region and gather times, step_ms and overlap (rank_fields).
+--rehearse-one-gpu runs the N > 1 entry with every rank on device 0 over gloo (a
+rehearsal of the driver's one-shot --gpus N run on a one-GPU box, not a measurement).
 Warmup: see settle() — untimed launches until the clock transient has passed.
 """
 from __future__ import annotations
@@ -79,7 +84,14 @@ def parse():
     ap.add_argument("--no-probe", action="store_true", help="skip the same-box streaming-read probe")
     ap.add_argument("--no-extras", action="store_true",
                     help="N = 1: skip the alternating-buffer and equal-work C4-shard legs (run after the timed region)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="N = 1: skip the configs leg (every other BASELINE config, tools/config_legs.py)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="REHEARSAL ONLY (N > 1 on a one-GPU box): every rank on device 0, a gloo process group, "
+                         "the gathers hop through host tensors; everything else is the production --gpus N path")
     a = ap.parse_args()
+    if a.rehearse_one_gpu and a.gpus < 2:
+        ap.error("--rehearse-one-gpu rehearses the N > 1 path: it needs --gpus >= 2")
     if a.packets_per_rank is None:
         a.packets_per_rank = default_packets_per_rank(a.gpus)
     return a
@@ -393,9 +405,13 @@ class Pipe:
     leg).  `gathered` (rank 0) holds 2 x world x every x n results: one half per group."""
 
     def __init__(self, W, shard, bufs, n, stream, do_gather, world, rank, gathered, dev, every=1, groups=2,
-                 helper=False):
+                 helper=False, host_hop=False):
         import torch
         self.W, self.shard, self.bufs, self.n, self.stream = W, shard, bufs, n, stream
+        # --rehearse-one-gpu (gloo): each group's results go to a host tensor before the
+        # gather (gloo gathers host tensors); `gathered` is then a host tensor on rank 0
+        self.host_hop = host_hop
+        self._hop_src = {}
         self.do_gather, self.world, self.rank, self.gathered = do_gather, world, rank, gathered
         self.K = max(1, int(every)) if do_gather else 1
         ng = max(2, int(groups)) if do_gather else 1
@@ -431,7 +447,7 @@ class Pipe:
         host clock from the issue to the work's future completing."""
         rec = self.gather_rec[-1]
         rec["work"] = work
-        if not hasattr(self.stream, "cuda_stream"):
+        if not hasattr(self.stream, "cuda_stream") or self.host_hop:
             rec["t0"] = time.perf_counter()
             work.get_future().then(lambda f, rec=rec: rec.__setitem__("t1", time.perf_counter()))
 
@@ -483,7 +499,12 @@ class Pipe:
             out = self.gathered[g * half:g * half + self.world * m * self.n]
         if self.timed:
             self.gather_rec.append({"steps": m})
-        if self.helper is not None:
+        if self.host_hop:  # rehearsal: device results -> host (waits for the CRC stream), gloo gather
+            with torch_stream(self.stream):
+                src = self.groups[g][:m * self.n].cpu()
+            self._hop_src[g] = src  # alive until the gather is waited for
+            self.works[g] = self.shard.gather_crcs_async(src, self.world, self.rank, out=out)
+        elif self.helper is not None:
             import torch
             self._hop(self.stream, self.helper)
             with torch.cuda.stream(self.helper):
@@ -540,6 +561,14 @@ class Pipe:
         return g.view(self.world, m * self.n)[:, (m - 1) * self.n:].reshape(-1)
 
 
+def torch_stream(stream):
+    """torch.cuda.stream(stream) for a HIP stream; no-op for the CPU tests' stand-in."""
+    import contextlib
+
+    import torch
+    return torch.cuda.stream(stream) if hasattr(stream, "cuda_stream") else contextlib.nullcontext()
+
+
 def time_steps(pipe: Pipe, steps: int, world: int, per_launch: bool = False):
     """Exactly `steps` steps, barrier + synchronize on both sides.  One HIP event pair on
     the CRC stream brackets the whole run (the gather runs on the collective's stream).
@@ -579,38 +608,50 @@ def time_steps(pipe: Pipe, steps: int, world: int, per_launch: bool = False):
     return kern, r0.elapsed_time(r1), el
 
 
-def rank_fields(kern_ms: list, gather_ms: list, el: float, steps: int, world: int, dev) -> tuple[float, dict]:
+def rank_fields(kern_ms: list, gather_ms: list, el: float, steps: int, world: int, dev,
+                region_ms: float | None = None) -> tuple[float, dict]:
     """The N > 1 line's per-rank fields (collectives: every rank must call this).  el =
-    this rank's wall seconds; returns (max over ranks of el, fields):
-      per_rank_kernel_ms, kernel_ms_max_over_ranks — mean CRC launch time per rank;
+    this rank's wall seconds and region_ms its CRC-stream event time, both from the timed
+    pass; kern_ms = per-launch times from the instrumented pass.  Returns (max over ranks
+    of el, fields):
+      per_rank_kernel_ms, kernel_ms_max_over_ranks — mean CRC launch time per rank
+        (instrumented pass);
+      per_rank_region_ms — the timed pass's CRC-stream time per step (its two events / K:
+        the launches plus any stream wait for a result slot);
       per_rank_gather_ms, gather_ms_max_over_ranks — mean duration of a gather collective
-        on its own stream (ProcessGroupNCCL's timing events, Pipe._time_gather);
-        gathers_per_rank = collectives timed in the timed region;
+        on its own stream (ProcessGroupNCCL's timing events, Pipe._time_gather; gloo: host
+        clock); gathers_per_rank = collectives timed in the timed region;
       step_ms — wall time per step (max over ranks);
-      overlap — step_ms - kernel_ms_max_over_ranks: the step time the kernels do not
-        explain.  About 0 when the gather hides behind the next CRC launches; about
-        gather_ms / gather_every when it serialises with them."""
+      overlap — step_ms - max(per_rank_region_ms), both from the timed pass: the step time
+        the CRC stream does not explain.  About 0 when the gather hides behind the next
+        CRC launches; about gather_ms / gather_every when it serialises with them.
+    The collectives run on `dev` with RCCL and on host tensors with gloo."""
     import torch
     import torch.distributed as dist
 
+    if dist.get_backend() == "gloo":
+        dev = torch.device("cpu")
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     km = sum(kern_ms) / len(kern_ms)
     gm = sum(gather_ms) / len(gather_ms) if gather_ms else 0.0
-    mine = torch.tensor([km, gm, float(len(gather_ms))], dtype=torch.float64, device=dev)
-    allr = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
+    rm = region_ms / steps if region_ms is not None else km
+    mine = torch.tensor([km, gm, float(len(gather_ms)), rm], dtype=torch.float64, device=dev)
+    allr = [torch.zeros(4, dtype=torch.float64, device=dev) for _ in range(world)]
     dist.all_gather(allr, mine)
     rows = [[float(v) for v in x.tolist()] for x in allr]
     per_k = [round(r[0], 5) for r in rows]
     per_g = [round(r[1], 5) for r in rows]
+    per_r = [round(r[3], 5) for r in rows]
     step_ms = round(el / steps * 1e3, 4)
     return el, {"per_rank_kernel_ms": per_k, "kernel_ms_max_over_ranks": max(per_k),
+                "per_rank_region_ms": per_r,
                 "per_rank_gather_ms": per_g, "gather_ms_max_over_ranks": max(per_g),
                 "gathers_per_rank": [int(r[2]) for r in rows],
-                "step_ms": step_ms, "overlap": round(step_ms - max(per_k), 5),
-                "overlap_rule": "step_ms - kernel_ms_max_over_ranks: ~0 = gather hidden behind the CRC launches, "
-                                "~gather_ms / gather_every = serialised"}
+                "step_ms": step_ms, "overlap": round(step_ms - max(per_r), 5),
+                "overlap_rule": "step_ms - max(per_rank_region_ms), both from the timed pass: ~0 = gather hidden "
+                                "behind the CRC launches, ~gather_ms / gather_every = serialised"}
 
 
 def kstats(kern: list, nbytes: int) -> dict:
@@ -671,7 +712,8 @@ def c4_shard_leg(W, shard, dev, local: int, steps: int, warmup: int, n: int = C4
     out.update(kstats(kern, nbytes))
     out["gather_ms"] = round(sum(gms) / len(gms), 5) if gms else None
     out["gathers"] = len(gms)
-    out["overlap"] = round(out["step_ms"] - out["kernel_ms_mean"], 5)
+    out["overlap"] = round(out["step_ms"] - out["region_ms_per_step"], 5)
+    out["overlap_rule"] = "step_ms - region_ms_per_step, both from the timed pass"
     del buf
     return out
 
@@ -735,10 +777,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    rehearse = args.rehearse_one_gpu  # every rank on device 0, gloo, gathers through host tensors
     if world > 1 or args.gather_n1:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(0 if rehearse else local)
         if world == 1:
             init_one_rank_group(local)
+        elif rehearse:
+            dist.init_process_group("gloo")
         else:
             os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")  # the gathers' own durations (Pipe.gather_ms)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -768,9 +813,10 @@ def main():
         W.reserve_cus(reserve, torch.cuda.current_device())
     every = args.gather_every if do_gather else 1
     ngroups = max(2, args.result_groups) if do_gather else 1
-    gathered = torch.empty(ngroups * world * every * n, dtype=torch.int32, device=dev) if do_gather and rank == 0 else None
+    gdev = torch.device("cpu") if rehearse else dev
+    gathered = torch.empty(ngroups * world * every * n, dtype=torch.int32, device=gdev) if do_gather and rank == 0 else None
     pipe = Pipe(W, shard, [buf], n, stream, do_gather, world, rank, gathered, dev, every=every, groups=ngroups,
-                helper=args.gather_helper)
+                helper=args.gather_helper and not rehearse, host_hop=rehearse and do_gather)
     out = torch.empty(n, dtype=torch.int32, device=dev)  # the read-probe leg's CRC launches
 
     def crc():
@@ -793,7 +839,7 @@ def main():
 
     per_rank = None
     if world > 1 or args.gather_n1:  # --gather-n1: the same fields from a one-rank RCCL world
-        el, per_rank = rank_fields(kern, gms, el, args.steps, world, dev)
+        el, per_rank = rank_fields(kern, gms, el, args.steps, world, dev, region_ms=region_ms)
 
     # parity of the WHOLE result vector (rank 0: the gathered vector when N > 1)
     parity = None
@@ -831,7 +877,8 @@ def main():
                            + (" + RCCL gather of u32 results to rank 0" if do_gather else ""),
                    "packets_per_rank": n, "payload_bytes": PAYLOAD, "global_packets": n * world,
                    "parallelism": f"packet shards x{world}" if world > 1 else "single GPU",
-                   "gather": ("RCCL gather to rank 0, overlapped with the next step's CRC" if do_gather else None),
+                   "gather": (("REHEARSAL: gloo gather of host copies to rank 0" if rehearse else
+                               "RCCL gather to rank 0, overlapped with the next step's CRC") if do_gather else None),
                    "gather_every": every if do_gather else None,
                    "result_groups": ngroups if do_gather else None,
                    "gather_helper_stream": bool(args.gather_helper) if do_gather else None,
@@ -839,7 +886,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_check": traffic_info,
                      "kernel": kernel_name, "kernel_ms_mean": round(kmean, 5),
-                     "kernel_ms_rule": "HIP events on the CRC stream around the timed region's K launches, / K",
+                     "kernel_ms_rule": "HIP events on the CRC stream around the timed region's K launches, / K"
+                                       + (" (with the gather this is the CRC stream's time per step: the launch "
+                                          "plus any wait for a free result slot)" if do_gather else ""),
                      "instrumented_pass": {"what": "the same K steps again, an event pair around every launch "
                                                    "(not part of value: ~5 us per step, profiles/r05v)",
                                            "kernel_ms_mean": round(kmean_pl, 5),
@@ -859,9 +908,21 @@ def main():
     }
     if per_rank is not None:
         line.update(per_rank)
+    if rehearse:
+        line["rehearsal"] = {"what": f"--rehearse-one-gpu: {world} ranks share device 0 over gloo; gathers hop "
+                                     "through host tensors. Exercises the --gpus N entry end to end; its timings "
+                                     "are NOT a scaling measurement",
+                             "backend": dist.get_backend()}
     extras = rank == 0 and world == 1 and not args.gather_n1 and n == 1 << 20 and not args.no_extras
     if extras:  # after the timed region and the probe: neither leg touches the headline numbers
         run_extra_legs(line, parity, W, shard, buf, nbytes, n, dev, local, stream, args)
+    if extras and not args.no_configs:  # every other BASELINE config, parity vs reference digests
+        torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import config_legs
+        line["configs"] = config_legs.run(W, TimingEvent)
+        if line["configs"]["parity_all"] is False:
+            parity["configs"] = False
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         hc = host_cores()
         threads = args.cpu_threads or hc["threads"]
@@ -871,7 +932,8 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
-    if parity is not None and (parity["match"] is False or parity.get("c4_shard_1gpu") is False):
+    if parity is not None and (parity["match"] is False or parity.get("c4_shard_1gpu") is False
+                               or parity.get("configs") is False):
         sys.exit("bench.py: result vector differs from the reference digest")
 
 

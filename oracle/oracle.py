@@ -74,6 +74,7 @@ def ref_lib() -> C.CDLL | None:
         r.ref_crc32.restype = C.c_uint32
         r.ref_crc32.argtypes = [C.c_void_p, C.c_size_t]
         r.ref_crc32_batch_fixed.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, _u32p]
+        r.ref_crc32_batch_var.argtypes = [C.c_void_p, _u64p, _u32p, C.c_size_t, _u32p]
         r.ref_crc32_batch_fixed_mt.restype = C.c_int
         r.ref_crc32_batch_fixed_mt.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, _u32p, C.c_int]
         _REF = r

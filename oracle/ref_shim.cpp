@@ -23,6 +23,13 @@ void ref_crc32_batch_fixed(const void *base, size_t stride, size_t len, size_t n
     for (size_t i = 0; i < n; ++i) out[i] = crc32(b + i * stride, len);
 }
 
+// Payloads at arbitrary offsets/lengths (config C5's packed mixed lengths): one reference
+// crc32 call per payload, as the receiver makes one per datagram (Receiver.cpp:32-33).
+void ref_crc32_batch_var(const void *base, const uint64_t *offs, const uint32_t *lens, size_t n, uint32_t *out) {
+    const char *b = static_cast<const char *>(base);
+    for (size_t i = 0; i < n; ++i) out[i] = crc32(b + offs[i], lens[i]);
+}
+
 int ref_crc32_batch_fixed_mt(const void *base, size_t stride, size_t len, size_t n, uint32_t *out,
                              int threads) {
     if (threads < 1) threads = 1;

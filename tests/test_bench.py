@@ -174,7 +174,7 @@ def test_n1_extra_legs_fields_on_cpu(monkeypatch, every):
     assert {"kernel_ms_mean", "GBs", "frac", "step_ms", "value_GiBs"} <= set(c4)
     # the timed gathers (full groups + the flushed partial one) and the step time beyond the kernel
     assert c4["gathers"] == -(-4 // every) and c4["gather_ms"] > 0
-    assert abs(c4["overlap"] - (c4["step_ms"] - c4["kernel_ms_mean"])) < 1e-4
+    assert abs(c4["overlap"] - (c4["step_ms"] - c4["region_ms_per_step"])) < 1e-4  # one pass
 
 
 def test_default_c4_leg_is_the_two_million_packet_shard():
@@ -250,3 +250,80 @@ def test_extra_leg_failure_is_reported_not_fatal(monkeypatch):
     monkeypatch.setattr(bench, "c4_shard_leg", lambda *a, **k: {"parity_match": False})
     bench.run_extra_legs(line, parity, None, None, None, 0, 0, "cpu", 0, None, args)
     assert parity["c4_shard_1gpu"] is False
+
+
+def test_rehearse_needs_more_than_one_gpu(monkeypatch):
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--rehearse-one-gpu"])
+    with pytest.raises(SystemExit):
+        bench.parse()
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--rehearse-one-gpu", "--steps", "3"])
+    a = bench.parse()
+    assert a.rehearse_one_gpu and a.packets_per_rank == 2 << 20  # the production per-rank shard
+
+
+def test_rehearsal_self_launch_keeps_the_flag(monkeypatch):
+    """The rehearsal goes through the production self-launch: the ranks re-parse the same
+    argv, flag included (read before any GPU call)."""
+    import bench
+    seen = {}
+    monkeypatch.setattr(subprocess, "call", lambda cmd: seen.setdefault("cmd", cmd) and 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--rehearse-one-gpu", "--steps", "3"])
+    with pytest.raises(SystemExit):
+        bench.main()
+    assert "--nproc-per-node=2" in seen["cmd"]
+    assert seen["cmd"][-5:] == ["--gpus", "2", "--rehearse-one-gpu", "--steps", "3"]
+
+
+def test_config_legs_zipf_is_the_oracle_generator():
+    """The configs leg restates oracle.zipf_lengths (it may not import the oracle); the
+    reference digests were made from the oracle's, so the two must agree bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import oracle as O
+    import config_legs
+    for n, s in ((1, 1.1), (1000, 1.0), (1 << 20, 1.1), (1 << 20, 1.0), (12345, 1.2)):
+        assert np.array_equal(config_legs.zipf_lengths(n, s=s), O.zipf_lengths(n, s=s)), (n, s)
+
+
+def test_config_digests_cover_every_row():
+    """Every configs-leg parity key has a reference digest (tests/golden/config_digests.json
+    from make_config_digests.py, bench_digests.json for the 1 M prefix)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import config_legs
+    D = config_legs.digests()
+    src = open(os.path.join(ROOT, "tools", "config_legs.py")).read()
+    for k in ("c2", "c3_1gib", "hostbuild_1gib", "build_1m", "1048576", "verify_fixup_1m"):
+        assert f'"{k}"' in src and len(D.get(k, "")) == 64, k
+    assert 'f"c5_zipf{s}"' in src
+    for k in ("c5_zipf1.1", "c5_zipf1.0"):
+        assert len(D.get(k, "")) == 64, k
+
+
+def test_config_digests_pinned_by_reference_on_small_prefix():
+    """Spot check of the digest recipe: the C2 digest is the 64 K prefix of the same
+    stream bench_digests.json's prefixes hash, recomputed here with the compiled reference
+    (or the oracle when oracle/_ref is absent)."""
+    import ctypes as C
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import oracle as O
+    import config_legs
+    n = 65536
+    buf = O.synth_fill_np(n * 1456)
+    ref = O.ref_lib()
+    out = np.zeros(n, np.uint32)
+    if ref is not None:
+        ref.ref_crc32_batch_fixed(buf.ctypes.data, 1456, 1456, n, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    else:
+        out = O.batch_fixed(buf, 1456, 1456, n)
+    assert hashlib.sha256(out.astype("<u4").tobytes()).hexdigest() == config_legs.digests()["c2"]
+
+
+def test_bench_product_legs_do_not_import_the_oracle():
+    """Only bench.py's cpu_baseline leg (and its no-digest spot check) may touch oracle/;
+    the configs leg checks parity against committed digests only."""
+    src = open(os.path.join(ROOT, "tools", "config_legs.py")).read()
+    assert "import oracle" not in src and "oracle/" not in src.replace("oracle/_ref", "")

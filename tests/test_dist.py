@@ -225,7 +225,7 @@ def test_gather_async_requires_out_on_dst():
         shard.gather_crcs_async(torch.zeros(4, dtype=torch.int32), 2, 0, out=torch.zeros(7, dtype=torch.int32))
 
 
-def _bench_pipe_worker(rank, world, port, every, steps, q, groups=2):
+def _bench_pipe_worker(rank, world, port, every, steps, q, groups=2, host_hop=False):
     """bench.py's own Pipe (results gathered in groups of `every` steps, two groups in
     flight, a partial group flushed at the end) over gloo, with a stand-in launch that
     writes rank * 1000 + step * 7 + lane into the step's result slot."""
@@ -249,7 +249,8 @@ def _bench_pipe_worker(rank, world, port, every, steps, q, groups=2):
             FakeW.calls += 1
 
     gathered = torch.empty(groups * world * every * n, dtype=torch.int32) if rank == 0 else None
-    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every, groups=groups)
+    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=every, groups=groups,
+                      host_hop=host_hop)
     seen = []
     real = S.gather_crcs_async
 
@@ -267,14 +268,18 @@ def _bench_pipe_worker(rank, world, port, every, steps, q, groups=2):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,every,steps,groups", [(2, 1, 3, 2), (2, 2, 5, 2), (3, 4, 6, 2), (8, 2, 5, 2),
-                                                      (2, 2, 9, 3), (3, 1, 7, 8)])
-def test_bench_pipe_grouped_gather(world, every, steps, groups):
+@pytest.mark.parametrize("world,every,steps,groups,host_hop", [(2, 1, 3, 2, False), (2, 2, 5, 2, False),
+                                                               (3, 4, 6, 2, False), (8, 2, 5, 2, False),
+                                                               (2, 2, 9, 3, False), (3, 1, 7, 8, False),
+                                                               (2, 2, 5, 2, True), (3, 1, 4, 2, True)])
+def test_bench_pipe_grouped_gather(world, every, steps, groups, host_hop):
+    """host_hop: the --rehearse-one-gpu form of the pipe (each group copied to a host
+    tensor, then a gloo gather), same vector and collectives."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_pipe_worker, args=(r, world, port, every, steps, q, groups))
+    procs = [ctx.Process(target=_bench_pipe_worker, args=(r, world, port, every, steps, q, groups, host_hop))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -330,7 +335,7 @@ def _rank_fields_worker(rank, world, port, every, steps, q):
     gms = pipe.gather_ms()
     kern, _, _ = bench.time_steps(pipe, steps, world, per_launch=True)  # the instrumented pass
     assert kern is not None and len(kern) == steps and region > 0
-    el_max, f = bench.rank_fields(kern, gms, el, steps, world, "cpu")
+    el_max, f = bench.rank_fields(kern, gms, el, steps, world, "cpu", region_ms=region)
     if rank == 0:
         q.put((f, el_max, el))
     dist.barrier()
@@ -341,7 +346,8 @@ def _rank_fields_worker(rank, world, port, every, steps, q):
 def test_bench_rank_fields_gather_and_overlap(world, every, steps):
     """The N > 1 line's overlap fields: per-rank gather time, gathers
     per rank (the timed region's collectives only: full groups plus the flushed partial
-    one), overlap = step_ms - kernel_ms_max_over_ranks, maxima consistent with the lists."""
+    one), overlap = step_ms - max(per_rank_region_ms) (both timed pass),
+    maxima consistent with the lists."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -359,4 +365,5 @@ def test_bench_rank_fields_gather_and_overlap(world, every, steps):
     assert f["kernel_ms_max_over_ranks"] == max(f["per_rank_kernel_ms"])
     assert f["gather_ms_max_over_ranks"] == max(f["per_rank_gather_ms"])
     assert el_max >= el0 and f["step_ms"] == round(el_max / steps * 1e3, 4)
-    assert abs(f["overlap"] - (f["step_ms"] - f["kernel_ms_max_over_ranks"])) < 1e-4
+    assert len(f["per_rank_region_ms"]) == world and all(r > 0 for r in f["per_rank_region_ms"])
+    assert abs(f["overlap"] - (f["step_ms"] - max(f["per_rank_region_ms"]))) < 1e-4

@@ -697,16 +697,25 @@ def test_packed_zipf_over_2gib_piece_ranges(W, broken):
     kernel in device-cut < 2 GiB sub-launches (launch_packed_ranges), not k_stream.  Every
     CRC equals the stream kernel's over the same batch (WTP_STREAM_KERNEL=1) and the oracle
     on the payloads around each 2 GiB - 64 KiB cut and a random sample.  broken: 40 pairs of
-    payloads swapped (offsets not packed) -> a sub-launch flags them and the gated k_stream
-    recomputes the batch; still exact."""
+    adjacent payloads swapped (these stay inside their sub-launch's view: computed there)
+    and one payload just before the first cut swapped with one ~5000 payloads past it,
+    which puts it outside its view (offsets not packed) -> that sub-launch flags it and the
+    gated k_stream recomputes the batch (status bit 3: its per-payload path ran); still
+    exact.  packed: no flag, k_stream returns at once (bit 3 clear)."""
     n = 17_000_000
     lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
     offs, lens = _packed(lens, first=3)
     rng = np.random.default_rng(17)
+    G = (1 << 31) - (1 << 16)
+    cut = int(np.searchsorted(offs, np.uint64(G - 3)))
     if broken:
         for b in np.sort(rng.choice(n - 2, 40, replace=False)):
             offs[[b, b + 1]] = offs[[b + 1, b]]
             lens[[b, b + 1]] = lens[[b + 1, b]]
+        a, b = cut - 5, cut + 5000
+        assert int(offs[b]) - G > (1 << 16)  # past the first sub-launch's < 2 GiB view
+        offs[[a, b]] = offs[[b, a]]
+        lens[[a, b]] = lens[[b, a]]
     total = int((offs + lens).max()) + 8
     assert total > (1 << 31)
     d = torch.empty(total, dtype=torch.uint8, device="cuda")
@@ -714,15 +723,15 @@ def test_packed_zipf_over_2gib_piece_ranges(W, broken):
     do = torch.from_numpy(offs.view(np.int64)).cuda()
     dl = torch.from_numpy(lens.view(np.int32)).cuda()
     out = u32_out(n)
+    W.device_status(0, clear=True)
     W.crc32_batch_packed(d, total, do, dl, n, out)
     assert W.LIB.wtp_last_kernel().decode().startswith("k_pieces<RangeArrayProvL, CrcEpi>")
+    assert bool(W.device_status(0, clear=True) & 8) == broken  # the gated k_stream's per-payload path
     got = to_u32(out, n)
     ref = u32_out(n)
     _forced_stream(W)(d, total, do, dl, n, ref)
     assert np.array_equal(got, to_u32(ref, n))
-    G = (1 << 31) - (1 << 16)
-    cut = int(np.searchsorted(offs, np.uint64(G - 3)))
-    idx = np.unique(np.concatenate([np.arange(cut - 3, cut + 3), [0, n - 1], rng.integers(0, n, 3000)]))
+    idx = np.unique(np.concatenate([np.arange(cut - 6, cut + 3), [0, n - 1, cut + 5000], rng.integers(0, n, 3000)]))
     host = d.cpu().numpy()
     del d
     want = O.batch_var(host, offs[idx], lens[idx])
@@ -816,6 +825,51 @@ def test_packed_over_2gib_graph_of_three_calls(W):
     for i in host_idx[:50]:
         i = int(i)
         assert int(got[i]) == O.crc32(d[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy()), i
+
+
+def test_packed_over_2gib_captured_on_torch_capture_stream(W):
+    """a packed >= 2 GiB call captured with torch.cuda.graph(g) and no
+    stream= (torch's shared default capture stream, never used eagerly) must capture, not
+    fail; and two such graphs, each over its own batch, replayed at once on two streams
+    must each give their own exact results (each captured call owns its descriptor slot)."""
+    n = 17_000_000
+    lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
+    offs, lens = _packed(lens)
+    total = int(offs[-1] + lens[-1])
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    ds = [torch.empty(total, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for k, d in enumerate(ds):
+        W.synth_fill(d, start_byte=k * 977)
+    outs = [u32_out(n) for _ in range(2)]
+    wants = []
+    for d in ds:
+        w = u32_out(n)
+        W.crc32_batch_packed(d, total, do, dl, n, w)
+        wants.append(w)
+    torch.cuda.synchronize()
+    assert not torch.equal(wants[0], wants[1])
+    graphs = []
+    for d, o in zip(ds, outs):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            W.crc32_batch_packed(d, total, do, dl, n, o)
+        graphs.append(g)
+    assert W.LIB.wtp_last_kernel().decode().startswith("k_pieces<RangeArrayProvL")
+    torch.cuda.synchronize()
+    for o in outs:
+        o.zero_()
+    torch.cuda.synchronize()
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    for rep in range(3):
+        for g, s in zip(graphs, ss):
+            with torch.cuda.stream(s):
+                g.replay()
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert torch.equal(outs[k], wants[k]), (rep, k)
+    i = int(n // 2)
+    assert int(to_u32(outs[1], n)[i]) == O.crc32(ds[1][int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy())
 
 
 def test_builder_slow_path_graph_of_three_calls(W):

@@ -158,7 +158,7 @@ def test_bench_pipelined_gather_one_rank(W):
     assert line["per_rank_kernel_ms"] == [line["kernel_ms_max_over_ranks"]] and line["kernel_ms_max_over_ranks"] > 0
     every = line["config"]["gather_every"]
     assert line["gathers_per_rank"] == [-(-5 // every)] and line["per_rank_gather_ms"][0] > 0  # full groups + the flushed one
-    assert abs(line["overlap"] - (line["step_ms"] - line["kernel_ms_max_over_ranks"])) < 1e-4
+    assert abs(line["overlap"] - (line["step_ms"] - max(line["per_rank_region_ms"]))) < 1e-4
 
 
 def test_bench_c4_shard_gather_one_rank(W):
@@ -188,10 +188,26 @@ def test_bench_n1_line_carries_equal_work_c4_leg(W):
     import sys
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "5", "--warmup", "5",
-                        "--no-cpu-baseline", "--no-probe"], capture_output=True, text=True, timeout=240)
+                        "--no-cpu-baseline", "--no-probe"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["config"]["packets_per_rank"] == 1 << 20 and line["parity"]["match"] is True
+    # the configs leg: every other BASELINE config, each row with its
+    # back-to-back and graph times, frac, and parity of the whole result vs a reference digest
+    cf = line["configs"]
+    assert cf["parity_all"] is True, json.dumps(cf)[:3000]
+    rows = {r["config"].split(":")[0]: r for r in cf["rows"]}
+    assert not any("error" in r for r in cf["rows"]), [r for r in cf["rows"] if "error" in r]
+    for name in ("C2", "C5", "verify", "build"):
+        dev_rows = [r for r in cf["rows"] if r["config"].startswith(name)]
+        assert dev_rows, name
+        for r in dev_rows:
+            assert r["b2b_ms"] > 0 and r["graph_ms"] > 0 and 0 < r["graph_frac"] <= 1.0, r
+            assert r["parity"]["match"] is True, r
+    assert sum(r["config"].startswith("C5") for r in cf["rows"]) == 3  # Zipf 1.1, 1.0, and k_stream forced
+    for name, legs in (("C3", ("pinned", "pageable")), ("hostbuild", ("pinned", "pinned_staged", "pageable"))):
+        for leg in legs:
+            assert rows[name][leg]["parity"]["match"] is True and rows[name][leg]["seconds"] > 0, (name, leg)
     c4 = line["c4_shard_1gpu"]
     assert c4["packets"] == 2097152 and c4["parity_match"] is True, c4
     assert c4["steps"] == 5 and 0 < c4["kernel_ms_mean"] <= c4["step_ms"] * 1.5
@@ -200,3 +216,30 @@ def test_bench_n1_line_carries_equal_work_c4_leg(W):
     # roofline.traffic depends on the committed PMC record, not on this run's results:
     # tests/test_bench.py::test_pmc_record_matches_shipped_kernel checks the record
     assert "traffic_check" in line["roofline"]
+
+
+def test_bench_rehearse_gpus2_end_to_end(W):
+    """the driver's one-shot `bench.py --gpus N` entry, rehearsed with
+    N = 2 on this one-GPU box: self-launch through torch.distributed.run, the WORLD_SIZE
+    check, per-rank synth_fill at rank * nbytes, reserve_cus, the real braided launches,
+    rank_fields' collectives and the gathered 2 x 2 M vector against the reference's
+    4,194,304-packet digest.  Only the device map (both ranks on device 0), the backend
+    (gloo) and the gather's host hop differ from production."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
+                        "--steps", "3"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["rehearsal"]["backend"] == "gloo"
+    assert line["config"]["packets_per_rank"] == 2097152 and line["config"]["global_packets"] == 4194304
+    assert line["config"]["reserved_cus"] == 8
+    assert line["parity"]["packets"] == 4194304 and line["parity"]["match"] is True, line["parity"]
+    for k in ("per_rank_kernel_ms", "per_rank_region_ms", "per_rank_gather_ms", "gathers_per_rank"):
+        assert len(line[k]) == 2, k
+    assert all(v > 0 for v in line["per_rank_kernel_ms"]) and all(v > 0 for v in line["per_rank_gather_ms"])
+    assert abs(line["overlap"] - (line["step_ms"] - max(line["per_rank_region_ms"]))) < 1e-4
+    assert line["value"] > 0 and line["steps"] == 3

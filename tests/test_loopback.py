@@ -272,7 +272,7 @@ def test_batched_receive_bench_gpu(binaries, cpu_max):
 
 
 
-@pytest.mark.parametrize("bad", ["64K", "abc", "-1", "99999999999999999999999"])
+@pytest.mark.parametrize("bad", ["64K", "abc", "-1", "+5", " 5", "\t65536", "\n7", "99999999999999999999999"])
 def test_verify_cpu_max_bytes_rejects_unparsable(binaries, bad):
     """WTP_VERIFY_CPU_MAX_BYTES must be a decimal byte count: strtoull would read '64K' or
     'abc' as 0 (the documented 'every batch to the GPU' setting), so the endpoint refuses

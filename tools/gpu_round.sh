@@ -88,6 +88,10 @@ for s in $STEPS; do
              -d "$OUT/profnox" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extras
            cd "$ROOT" ;;
     pmcnew) pmc_refresh ;;
+    c4ab)  run c4ab 600 python -u tools/c4_leg_ab.py --rounds ${C4AB_ROUNDS:-8} --steps 20 --out "$OUT/c4_leg_ab.json" ;;
+    rehearse) run rehearse 400 python bench.py --gpus 2 --rehearse-one-gpu --steps 20 --warmup 5 ;;
+    newtests) run gpu_tests_new 600 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread \
+             -k "rehearse or captured_on_torch or piece_ranges or equal_work_c4_leg or pipelined_gather_one_rank" ;;
     gev)   for k in ${GEV:-1 2 4}; do
              run "c4gather_k$k" 300 python bench.py --steps 20 --warmup 5 --gather-n1 --packets-per-rank 2097152 --gather-every $k --no-cpu-baseline --no-probe
            done ;;
