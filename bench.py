@@ -248,27 +248,38 @@ def self_launch(args) -> None:
     sys.exit(subprocess.call(cmd))
 
 
-def settle(step, stream, w_req: int, block: int = 25, tol: float = 0.01, floor: int = 100, cap_s: float = 3.0):
+def settle(step, stream, w_req: int, block: int = 25, tol: float = 0.01, floor: int = 100, cap_s: float = 3.0,
+           world: int = 1, flag_dev=None):
     """Untimed warmup: at least max(w_req, floor) launches, then until the mean launch
     time of three consecutive blocks of `block` launches agrees within `tol` (cap
     cap_s seconds).  A cold MI355X runs this kernel fast for ~5 launches, then the
     power controller pulls the clock down for launches ~5-50 (262 us vs 219 us steady,
-    profiles/r02a/transient.json); a fixed 5-launch warmup times exactly that dip."""
+    profiles/r02a/transient.json); a fixed 5-launch warmup times exactly that dip.
+    world > 1: the stop decision is collective (all_reduce MAX of "keep going" on
+    flag_dev after every block), so every rank runs the same number of steps.  With the
+    gather, steps decide the collectives each rank issues: a rank-local count let rank 0
+    flush a partial result group that rank 1 gathered whole, a mismatched gather
+    (found by the --rehearse-one-gpu run, profiles/r06a)."""
     import torch
 
     means, done, t0 = [], 0, time.perf_counter()
     while True:
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s, e = TimingEvent(), TimingEvent()
         s.record(stream)
         for _ in range(block):
             step()
         e.record(stream)
-        e.synchronize()
+        torch.cuda.synchronize()
         done += block
         means.append(s.elapsed_time(e) / block * 1e3)
-        if done >= max(w_req, floor) and len(means) >= 3 and max(means[-3:]) <= (1 + tol) * min(means[-3:]):
-            break
-        if time.perf_counter() - t0 > cap_s and done >= w_req:
+        stop = (done >= max(w_req, floor) and len(means) >= 3 and max(means[-3:]) <= (1 + tol) * min(means[-3:])) \
+            or (time.perf_counter() - t0 > cap_s and done >= w_req)
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([0 if stop else 1], dtype=torch.int32, device=flag_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            stop = int(t.item()) == 0
+        if stop:
             break
     return done, [round(m, 1) for m in means]
 
@@ -822,7 +833,8 @@ def main():
     def crc():
         W.crc32_batch_fixed(buf, PAYLOAD, PAYLOAD, n, out, stream)
 
-    warm_done, warm_means = settle(pipe.step, stream, args.warmup)
+    warm_done, warm_means = settle(pipe.step, stream, args.warmup, world=world,
+                                   flag_dev=torch.device("cpu") if rehearse else dev)
     pipe.drain()
     torch.cuda.synchronize()
 

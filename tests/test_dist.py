@@ -367,3 +367,59 @@ def test_bench_rank_fields_gather_and_overlap(world, every, steps):
     assert el_max >= el0 and f["step_ms"] == round(el_max / steps * 1e3, 4)
     assert len(f["per_rank_region_ms"]) == world and all(r > 0 for r in f["per_rank_region_ms"])
     assert abs(f["overlap"] - (f["step_ms"] - max(f["per_rank_region_ms"]))) < 1e-4
+
+
+def _settle_worker(rank, world, port, q):
+    """bench.settle over gloo with rank-dependent launch times: rank 0's settle within
+    three blocks, rank 1's never (noisy) until the cap.  The stop decision must be
+    collective, or the ranks' Pipes issue different gathers (r06a: a partial group on
+    one rank, a whole one on the other -> gloo size mismatch; RCCL would hang)."""
+    import random
+    import time as _t
+
+    import torch
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "a3-reliable-transport_amd")):
+        sys.path.insert(0, p)
+    import bench
+    import shard as S
+    bench.TimingEvent = _WallEvent
+    torch.cuda.synchronize = lambda *a: None
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 64
+
+    class FakeW:
+        def crc32_batch_fixed(self, buf, stride, length, nn, out, stream=None):
+            _t.sleep(0.001 if rank == 0 else random.choice((0.0005, 0.003)))
+            out.copy_(torch.arange(nn, dtype=torch.int32) + rank)
+
+    gathered = torch.empty(2 * world * 2 * n, dtype=torch.int32) if rank == 0 else None
+    pipe = bench.Pipe(FakeW(), S, [None], n, "stream", True, world, rank, gathered, "cpu", every=2)
+    done, _ = bench.settle(pipe.step, "stream", 5, block=5, floor=10, cap_s=0.6, world=world, flag_dev="cpu")
+    pipe.drain()
+    _, _, el = bench.time_steps(pipe, 3, world)
+    alld = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(alld, torch.tensor([done]))
+    if rank == 0:
+        q.put(([int(x) for x in alld], pipe.gathered_vector().numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_settle_is_collective_with_uneven_ranks():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_settle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    dones, vec = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert dones[0] == dones[1]  # one step count on every rank, so the same gathers
+    assert np.array_equal(vec, np.concatenate([np.arange(64) + r for r in range(2)]).astype(np.int32))

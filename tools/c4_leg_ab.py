@@ -11,6 +11,9 @@ the same 2 M x 1456 B shard (rank 0's C4 shard), `--steps` steps like the driver
               giving both kernel_ms and step_ms (bench.time_steps(per_launch=True))
   plain       no gather, no Pipe: 2 M launches on a side stream with 8 reserved CUs, an
               event pair per launch (kernel_ms) and one pair around the run (region)
+  pipe_nogather  bench.Pipe without the gather (side stream, 8 reserved CUs): the Pipe's own
+              cost, so plain vs pipe_nogather vs head splits the gap into Pipe and gather
+  head_every4 head with the results of 4 steps per gather (half the collectives)
 
 Every variant with a process group makes its own one-rank RCCL group (fresh port) and
 destroys it.  Prints one JSON line per run and a summary (medians over rounds).
@@ -44,10 +47,10 @@ def fresh_port():
     os.environ["MASTER_PORT"] = str(p)
 
 
-def head(steps, timing):
+def head(steps, timing, every=2):
     os.environ["TORCH_NCCL_ENABLE_TIMING"] = "1" if timing else "0"
     fresh_port()
-    r = bench.c4_shard_leg(W, shard, torch.device("cuda", 0), 0, steps, 5, every=2, groups=2)
+    r = bench.c4_shard_leg(W, shard, torch.device("cuda", 0), 0, steps, 5, every=every, groups=2)
     return {"kernel_ms": r["kernel_ms_mean"], "kernel_median_ms": r["kernel_ms_median"], "step_ms": r["step_ms"],
             "region_ms": r["region_ms_per_step"], "parity": r["parity_match"]}
 
@@ -74,6 +77,25 @@ def r04pipe(steps, buf):
         W.reserve_cus(0, 0)
         torch.cuda.set_stream(prev)
         dist.destroy_process_group()
+    ks = sorted(kern)
+    return {"kernel_ms": sum(ks) / len(ks), "kernel_median_ms": ks[len(ks) // 2], "step_ms": el / steps * 1e3,
+            "region_ms": region / steps, "parity": par}
+
+
+def pipe_nogather(steps, buf):
+    """bench.Pipe without the gather on a side stream, 8 reserved CUs: the pipe's own cost."""
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream()
+    W.reserve_cus(8, 0)
+    try:
+        pipe = bench.Pipe(W, None, [buf], N, st, False, 1, 0, None, dev)
+        bench.settle(pipe.step, st, 5)
+        torch.cuda.synchronize()
+        _, region, el = bench.time_steps(pipe, steps, 1)
+        kern, _, _ = bench.time_steps(pipe, steps, 1, per_launch=True)
+        par = bench.parity_digest(pipe.last_out().cpu().numpy().view(np.uint32))["match"]
+    finally:
+        W.reserve_cus(0, 0)
     ks = sorted(kern)
     return {"kernel_ms": sum(ks) / len(ks), "kernel_median_ms": ks[len(ks) // 2], "step_ms": el / steps * 1e3,
             "region_ms": region / steps, "parity": par}
@@ -122,7 +144,8 @@ def main():
     buf = torch.empty(N * P + 64, dtype=torch.uint8, device="cuda")
     W.synth_fill(buf, nbytes=N * P)
     variants = {"head": lambda: head(a.steps, True), "head_notime": lambda: head(a.steps, False),
-                "r04pipe": lambda: r04pipe(a.steps, buf), "plain": lambda: plain(a.steps, buf)}
+                "r04pipe": lambda: r04pipe(a.steps, buf), "plain": lambda: plain(a.steps, buf),
+                "pipe_nogather": lambda: pipe_nogather(a.steps, buf), "head_every4": lambda: head(a.steps, True, 4)}
     names = list(variants)
     runs = []
     for r in range(a.rounds):
