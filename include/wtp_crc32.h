@@ -126,11 +126,12 @@ int wtp_crc32_batch_var(const void *d_base, size_t base_bytes, const uint64_t *d
    or above 2 GiB the general kernel in sub-launches over < 2 GiB views that the device
    cuts from the offsets; a sub-launch that meets a payload outside its
    view (offsets not packed) flags it and the stream kernel then recomputes the batch,
-   so results stay exact for any offsets.  That route keeps 32 KiB of device scratch per
-   stream, made on the stream's first such call, which must not be inside a graph
-   capture (a captured call reuses it: replay such a graph only where no other call of
-   this route runs on its capture stream at the same time).  WTP_STREAM_KERNEL=1 in the
-   environment forces the stream kernel. */
+   so results stay exact for any offsets.  That route keeps its descriptors in device
+   scratch: 32 KiB per stream outside graph capture (made on the stream's first such
+   call); a call captured into a graph takes one of 64 slots made at init, its own for
+   the life of the process, so graphs captured on one stream may be replayed
+   concurrently; with every slot taken a captured call runs the stream kernel (exact).
+   WTP_STREAM_KERNEL=1 in the environment forces the stream kernel. */
 int wtp_crc32_batch_packed(const void *d_base, size_t base_bytes, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, size_t n, uint32_t *d_out, void *stream);
 
