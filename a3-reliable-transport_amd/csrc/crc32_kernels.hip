@@ -195,7 +195,7 @@ struct StagSet {
 // its first data loads, since vmcnt completes in order and the table writes would
 // otherwise wait for the first round's data (the fill ended 4.4 us after entry).
 #ifndef WTP_FILL_X4_PC
-#define WTP_FILL_X4_PC 0  // the same for the piece kernel's 1024-thread fill (A/B builds)
+#define WTP_FILL_X4_PC 1  // the same for the piece kernel's 1024-thread fill: C5 -0.5..0.8%, 64 K mixed -3% (r06c)
 #endif
 #ifndef WTP_FILL_X4
 #define WTP_FILL_X4 1  // 16-B table loads, each feeding 4 stores (<= 512 threads; 0: one dword per store, A/B builds)
@@ -208,7 +208,9 @@ struct StagFill {
     // 16-B LDS stores (each 8-lane group still writes 128 contiguous bytes of one row).
     // A quarter of the prologue's vector memory instructions: C2 (64 K packets) 15.46 ->
     // 14.29 us from a graph, 16 K 7.03 -> 5.98, 1 M 216.5 -> 214.9 (interleaved,
-    // profiles/r04fx).
+    // profiles/r04fx).  The piece kernel's 1024-thread fill too since round 6 (7 -> 4 loads
+    // per thread): C5 1 M 47.4 -> 47.0-47.2 us median, 64 K mixed 19.2 -> 18.6-18.7
+    // (interleaved, both library orders, profiles/r06c).
     static constexpr bool kX4 = WTP_FILL_X4 && (THREADS <= 512 || WTP_FILL_X4_PC);
     static constexpr int PER = kX4 ? NS * 512 / THREADS : NS * 2048 / THREADS;  // loads per thread
     typename std::conditional<kX4, u32x4, uint32_t>::type v[PER];
@@ -1575,8 +1577,8 @@ static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && 
                   WTP_PC_TAILCLAMP == 0,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
-static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 0,
-              "product build: held results every 16 flushes, 16-B table fill (braided kernels)");
+static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 1,
+              "product build: held results every 16 flushes, 16-B table fill (braided and piece kernels)");
 static_assert(WTP_BUILD_THREADS == 128 && WTP_BUILD_DIAG == 0 && WTP_BUILD_DEPTH == 2 && WTP_BUILD_SAUX == 2 &&
                   WTP_BUILD_WLEAD == 1 && WTP_BUILD_LAUX == 2 && WTP_BUILD_SAUX0 == 0,
               "product build: fused-builder knobs must keep their shipped values");

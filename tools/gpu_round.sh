@@ -150,6 +150,12 @@ for s in $STEPS; do
     abbuild) run abbuild 300 python tools/ab_lib.py --what build ${AB_LIBS} ;;
     abcrc) run abcrc 300 python tools/ab_lib.py --what crc --n ${AB_N:-1048576} ${AB_LIBS} ;;
     abc5) run abc5 300 python tools/ab_lib.py --what c5 ${AB_LIBS:-a3-reliable-transport_amd/lib/libwtp_crc32.so} ;;
+    abc5x) # both library orders, 1 M and 64 K payloads (AB_LIBS = two libraries)
+           set -- ${AB_LIBS}
+           for nn in 1048576 65536; do
+             run "abc5_n${nn}_fwd" 300 python tools/ab_lib.py --what c5 --rounds 30 --n $nn $1 $2
+             run "abc5_n${nn}_rev" 300 python tools/ab_lib.py --what c5 --rounds 30 --n $nn $2 $1
+           done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kbalt) for al in 0 1; do  # braided kernel, its ablations and the probes: one buffer vs alternating buffers
              KB_ALT=$al KB_ONLY="${KB_VARS:-braid512_prod,braid512_skel,braid512_nolut,braid512_nofold,braid512_noprio,read_probe_g256x512,strided_nt_d2_g512}" \
