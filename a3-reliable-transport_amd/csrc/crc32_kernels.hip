@@ -74,7 +74,8 @@ constexpr uint32_t OFF_T256 = OFF_HINIT + kHinitWords;
 constexpr uint32_t kStNibOps = 6 + 32;
 constexpr uint32_t OFF_NIB = OFF_T256 + 1024;
 constexpr uint32_t OFF_X64 = OFF_NIB + kStNibOps * 128;  // x^(8*64): joins the two chains of a 128-B piece
-constexpr uint32_t TAB_WORDS = OFF_X64 + 1024;
+constexpr uint32_t OFF_S8 = OFF_X64 + 1024;  // 4x256 word tables, a word then 4 zero bytes (split piece chains)
+constexpr uint32_t TAB_WORDS = OFF_S8 + 1024;
 
 // LDS images (staggered table sets are described at StagKeys below).
 constexpr uint32_t kOpBytes = 4096;  // a plain operator: 4 byte tables x 256 words
@@ -310,6 +311,16 @@ __device__ __forceinline__ uint32_t stag_apply3(const char *lds, const uint32_t 
     const uint32_t a2 = __builtin_amdgcn_perm(x, key[2], sel[2]);
     const uint32_t a3 = __builtin_amdgcn_perm(x, key[3], sel[3]);
     return xor3(lds_rd(lds, a0 + OFF), lds_rd(lds, a1 + OFF), lds_rd(lds, a2 + OFF)) ^ lds_rd(lds, a3 + OFF);
+}
+
+// Operator stored as 8 nibble tables of 16 words at LDS byte address `base` (which may
+// differ per lane): f(v) = XOR_i N_i[(v >> 4i) & 15].  A table's 16 words sit in 16
+// consecutive banks, so a wave-uniform operator never conflicts.
+__device__ __forceinline__ uint32_t nib_apply(const char *lds, uint32_t base, uint32_t v) {
+    uint32_t l[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) l[i] = lds_rd(lds, base + 64u * i + 4u * __builtin_amdgcn_ubfe(v, 4 * i, 4));
+    return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
 }
 
 // Wave issue priority, rotated (general kernel).  The SIMD arbiter favours the oldest of
@@ -904,7 +915,17 @@ constexpr uint32_t kPcWords = uint32_t(kPieceS) / 4;                // window wo
 constexpr uint32_t kPcNOps = kPieceS == 64 ? 5 : 6;                  // plain scan operators in LDS
 constexpr uint32_t kPcOps = 65536;
 constexpr uint32_t kPcHinit = kPcOps + kPcNOps * kOpBytes;
-constexpr uint32_t kPcStage = kPcHinit + 4 * kHinitWords;
+// WTP_PC_SPLIT (A/B knob, off): each lane's 64-B window as two interleaved chains (even /
+// odd words) over word tables that advance 8 bytes (region 0, set 0 = S8 instead of S4),
+// the odd chain's last word through a nibble-table S4 operator (512 B): 8 dependent LDS
+// round trips per round instead of 16, for +13 VALU and +4 lookups per lane.  Bit-exact
+// (342 GPU tests), but C5 got ~2% slower (46.0 -> 46.9, 45.7 -> 46.6 us, both library
+// orders, profiles/r06e): the loop is bound by VALU issue, not by its LDS chain latency.
+#ifndef WTP_PC_SPLIT
+#define WTP_PC_SPLIT 0
+#endif
+constexpr uint32_t kPcNib4 = (kPcHinit + 4 * kHinitWords + 15) & ~15u;
+constexpr uint32_t kPcStage = WTP_PC_SPLIT ? kPcNib4 + 512 : kPcHinit + 4 * kHinitWords;
 constexpr uint32_t kPcChunks = 4 * uint32_t(kPieceS) + 16;  // span chunks a slot holds: 64 pieces + gaps + head slack
 constexpr uint32_t kPcSlot = 16 * (kPcChunks + kPcChunks / 16 + 1);  // windows read one chunk past
 constexpr uint32_t kPcSpanRegs = (kPcChunks + 63) / 64;     // lane-contiguous 16-B loads per span
@@ -919,6 +940,7 @@ constexpr uint32_t kPcLdsWords = (kPcRem + 64) / 4;      // 161,904 B
 static_assert(kPcRem % 16 == 0 && kPcStage % 16 == 0 && kPcSlot % 16 == 0 && kPcOps % 16 == 0, "LDS vector alignment");
 static_assert(16 * (kPcChunks + kPcChunks / 16 + 1) <= kPcSlot, "staging slot");
 static_assert(kPcLdsWords * 4 <= 163840, "LDS");
+static_assert(!WTP_PC_SPLIT || kPieceS == 64, "split chains: 64-B pieces");
 
 __device__ __forceinline__ uint32_t stage_addr(uint32_t chunk) { return 16u * (chunk + (chunk >> 4)); }
 
@@ -1377,7 +1399,9 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
         for (int i = 0; i < int(kPcWords) + 1; ++i) e[i] = e[i] ^ ((e[i] ^ e[i + 1]) & m1);
 
         // one chain per 64 B of the window (128-B pieces: two independent chains, joined
-        // below by x^(8*64))
+        // below by x^(8*64)); WTP_PC_SPLIT: two interleaved chains per 64 B (below)
+        uint32_t c;
+        if constexpr (!WTP_PC_SPLIT) {
         constexpr int kChains = int(kPcWords) / 16;
         uint32_t cc[kChains];
         cc[0] = (lane == 0u) ? carry : 0u;  // carry is 0 unless packet p0 continues
@@ -1386,7 +1410,7 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
         for (int j = 0; j < 16 * kChains; ++j) {
             const int i = (j % kChains) * 16 + j / kChains;  // interleave the chains
-            uint32_t &c = cc[j % kChains];
+            uint32_t &cj = cc[j % kChains];
             const uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
             // keep the bytes at window offset >= vf: the low s = clamp(8 vf - 32 i, 0, 32)
             // bits of word i go.  One v_med3 + one v_lshlrev_b64 (the shift unit reads 6
@@ -1395,10 +1419,31 @@ __device__ __forceinline__ void pieces_loop(char *lds, __amdgpu_buffer_rsrc_t rs
             const int32_t t = vf8 < 32 * i ? 32 * i : (vf8 > 32 * i + 32 ? 32 * i + 32 : vf8);
             const uint64_t k64 = uint64_t(0xFFFFFFFFu) << (uint32_t(t) & 63u);
             const uint32_t keep = (i & 1) ? uint32_t(k64 >> 32) : uint32_t(k64);
-            c = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(c, wd, keep, 0x78));  // c ^ (wd & keep)
+            cj = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(cj, wd, keep, 0x78));  // cj ^ (wd & keep)
         }
-        uint32_t c = cc[0];
+        c = cc[0];
         if constexpr (kChains == 2) c = stag_apply3x<128>(lds, K.kA, K.sel, cc[0], cc[1]);  // x^(8*64) * c0 ^ c1
+        } else {
+            // two chains, 8 dependent steps each: even words advance by S8 (a word then 4
+            // zero bytes, the odd word's slot) and end aligned with the window's end; odd
+            // words 1..13 likewise, and word 15 by a plain S4 step (nibble tables)
+            uint32_t ca = (lane == 0u) ? carry : 0u, cb = 0u;
+            const int32_t vf8 = 8 * vf;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t wd = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
+                const int32_t t = vf8 < 32 * i ? 32 * i : (vf8 > 32 * i + 32 ? 32 * i + 32 : vf8);
+                const uint64_t k64 = uint64_t(0xFFFFFFFFu) << (uint32_t(t) & 63u);
+                const uint32_t keep = (i & 1) ? uint32_t(k64 >> 32) : uint32_t(k64);
+                if ((i & 1) == 0)
+                    ca = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(ca, wd, keep, 0x78));
+                else if (i < 15)
+                    cb = stag_apply3<0>(lds, K.kA, K.sel, __builtin_amdgcn_bitop3_b32(cb, wd, keep, 0x78));
+                else
+                    cb = nib_apply(lds, kPcNib4, __builtin_amdgcn_bitop3_b32(cb, wd, keep, 0x78));
+            }
+            c = ca ^ cb;
+        }
         // head piece: R_~0(head) = R_0(0^vf || head) ^ shift(~0, S - vf)
         const uint32_t hw = lds_rd(lds, kPcHinit + 4u * uint32_t(kPieceS - (vf < 0 ? 0 : vf)));
         c ^= gp == 0u ? hw : 0u;
@@ -1461,8 +1506,9 @@ struct PcTables {
     StagFill<2, THREADS> fill;
     u32x4 q[kOpPer];
     uint32_t hv;
+    u32x4 n4;
     __device__ __forceinline__ static void sets(const uint32_t *gtab, StagSet (&s)[2]) {
-        s[0] = {gtab + OFF_S4, 0u};
+        s[0] = {gtab + (WTP_PC_SPLIT ? OFF_S8 : OFF_S4), 0u};
         s[1] = {gtab + (kPieceS == 64 ? OFF_FWD : OFF_X64), 128u};  // x^(8*64)
     }
     __device__ __forceinline__ void load(const uint32_t *gtab) {
@@ -1476,6 +1522,8 @@ struct PcTables {
             q[k] = src[i < kOpQ ? i : 0];
         }
         hv = gtab[OFF_HINIT + (threadIdx.x <= kPieceS ? threadIdx.x : 0)];
+        if constexpr (WTP_PC_SPLIT)  // nibble-table S4 (shift by 4 bytes): operator 6 + 4 of OFF_NIB
+            n4 = reinterpret_cast<const u32x4 *>(gtab + OFF_NIB + 128 * 10)[threadIdx.x & 31u];
     }
     __device__ __forceinline__ void store(char *lds, const uint32_t *gtab) const {
         StagSet ss[2];
@@ -1488,6 +1536,8 @@ struct PcTables {
             if (i < kOpQ) dst[i] = q[k];
         }
         if (threadIdx.x <= kPieceS) reinterpret_cast<uint32_t *>(lds + kPcHinit)[threadIdx.x] = hv;
+        if constexpr (WTP_PC_SPLIT)
+            if (threadIdx.x < 32u) reinterpret_cast<u32x4 *>(lds + kPcNib4)[threadIdx.x] = n4;
     }
 };
 
@@ -1574,7 +1624,7 @@ static_assert(kVfPass <= kVfCap && kVfCtl + 64 <= kBraidLdsWords * 4, "verify fi
 // compile error, not a library that runs wrong.
 #ifndef WTP_AB_BUILD
 static_assert(WTP_PC_S == 64 && WTP_PC_THREADS == 1024 && WTP_PC_LEN128 == 1 && WTP_PC_LAG == 1 && WTP_PC_DMA == 1 &&
-                  WTP_PC_TAILCLAMP == 0,
+                  WTP_PC_TAILCLAMP == 0 && WTP_PC_SPLIT == 0,
               "product build: piece-kernel knobs must keep their shipped values");
 static_assert(WTP_BR_PROLOGUE_DIAG == 0 && WTP_PROBE == 0, "product build: no probe / prologue ablation");
 static_assert(WTP_BR_HOLD == 16 && WTP_FILL_X4 == 1 && WTP_FILL_X4_PC == 1,
@@ -1715,15 +1765,6 @@ constexpr uint32_t kStLdsWords = (kStBal + (kStWaves + 1) * 8) / 4;
 constexpr uint32_t kStMaxLen = 4095;  // the length shift has four 3-bit levels
 static_assert(kStLdsWords * 4 <= 163840, "k_stream LDS");
 
-// Operator stored as 8 nibble tables of 16 words at LDS byte address `base` (which may
-// differ per lane): f(v) = XOR_i N_i[(v >> 4i) & 15].  A table's 16 words sit in 16
-// consecutive banks, so a wave-uniform operator never conflicts.
-__device__ __forceinline__ uint32_t nib_apply(const char *lds, uint32_t base, uint32_t v) {
-    uint32_t l[8];
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) l[i] = lds_rd(lds, base + 64u * i + 4u * __builtin_amdgcn_ubfe(v, 4 * i, 4));
-    return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
-}
 
 // P at round position x (0 <= x < kStRound): lane x/128's anchor for the 32-B block
 // holding x, fed with the t = x % 32 block bytes before x (whole words by slice-by-4,
@@ -2174,6 +2215,7 @@ std::vector<uint32_t> host_tables() {
     }
     for (uint32_t h = 0; h <= uint32_t(kPieceS); ++h) t[OFF_HINIT + h] = shift_bytes(0xFFFFFFFFu, h);
     make_operator(&t[OFF_X64], [](uint32_t v) { return shift_bytes(v, 64); });
+    make_word_tables(&t[OFF_S8], 8);
     make_operator(&t[OFF_T256], [](uint32_t v) { return shift_bytes(v, 32); });
     auto nib = [&](uint32_t op, uint64_t nbytes) {
         for (uint32_t i = 0; i < 8; ++i)

@@ -218,28 +218,29 @@ def test_bench_n1_line_carries_equal_work_c4_leg(W):
     assert "traffic_check" in line["roofline"]
 
 
-def test_bench_rehearse_gpus2_end_to_end(W):
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_bench_rehearse_gpus2_end_to_end(W, gpus):
     """the driver's one-shot `bench.py --gpus N` entry, rehearsed with
-    N = 2 on this one-GPU box: self-launch through torch.distributed.run, the WORLD_SIZE
+    N = 2 and 4 on this one-GPU box: self-launch through torch.distributed.run, the WORLD_SIZE
     check, per-rank synth_fill at rank * nbytes, reserve_cus, the real braided launches,
-    rank_fields' collectives and the gathered 2 x 2 M vector against the reference's
-    4,194,304-packet digest.  Only the device map (both ranks on device 0), the backend
+    rank_fields' collectives and the gathered N x 2 M vector against the reference's
+    4 M / 8 M-packet digest.  Only the device map (both ranks on device 0), the backend
     (gloo) and the gather's host hop differ from production."""
     import json
     import subprocess
     import sys
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--rehearse-one-gpu",
                         "--steps", "3"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["rehearsal"]["backend"] == "gloo"
-    assert line["config"]["packets_per_rank"] == 2097152 and line["config"]["global_packets"] == 4194304
+    assert line["n_gpus"] == gpus and line["rehearsal"]["backend"] == "gloo"
+    assert line["config"]["packets_per_rank"] == 2097152 and line["config"]["global_packets"] == gpus * 2097152
     assert line["config"]["reserved_cus"] == 8
-    assert line["parity"]["packets"] == 4194304 and line["parity"]["match"] is True, line["parity"]
+    assert line["parity"]["packets"] == gpus * 2097152 and line["parity"]["match"] is True, line["parity"]
     for k in ("per_rank_kernel_ms", "per_rank_region_ms", "per_rank_gather_ms", "gathers_per_rank"):
-        assert len(line[k]) == 2, k
+        assert len(line[k]) == gpus, k
     assert all(v > 0 for v in line["per_rank_kernel_ms"]) and all(v > 0 for v in line["per_rank_gather_ms"])
     assert abs(line["overlap"] - (line["step_ms"] - max(line["per_rank_region_ms"]))) < 1e-4
     assert line["value"] > 0 and line["steps"] == 3
