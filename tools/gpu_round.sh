@@ -88,6 +88,17 @@ for s in $STEPS; do
              -d "$OUT/profnox" -o bench -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extras
            cd "$ROOT" ;;
     pmcnew) pmc_refresh ;;
+    pmccfg) # FETCH_SIZE and WRITE_SIZE of every configs-leg kernel, one config per process and pass
+           cd /tmp
+           for row in c2 c5_1.1 c5_1.0 verify build; do
+             for ctr in FETCH_SIZE WRITE_SIZE; do
+               run "pmc_${row}_${ctr}" 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmccfg/$row" -o "${row}_${ctr}" \
+                 -- python3 "$ROOT/tools/pmc_configs.py" $row 20
+             done
+           done
+           cd "$ROOT"
+           python3 tools/pmc_configs.py --summarize "$OUT/pmc_configs.json" $(for row in c2 c5_1.1 c5_1.0 verify build; do echo "$row=$OUT/pmccfg/$row"; done) \
+             > "$OUT/pmc_configs.log" 2>&1 || true ;;
     c4ab)  run c4ab 600 python -u tools/c4_leg_ab.py --rounds ${C4AB_ROUNDS:-8} --steps 20 --out "$OUT/c4_leg_ab.json" ;;
     rehearse) run rehearse 400 python bench.py --gpus 2 --rehearse-one-gpu --steps 20 --warmup 5 ;;
     newtests) run gpu_tests_new 600 python -u -m pytest tests -m gpu -v -rf --timeout=300 --timeout-method thread \
