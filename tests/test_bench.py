@@ -327,3 +327,31 @@ def test_bench_product_legs_do_not_import_the_oracle():
     the configs leg checks parity against committed digests only."""
     src = open(os.path.join(ROOT, "tools", "config_legs.py")).read()
     assert "import oracle" not in src and "oracle/" not in src.replace("oracle/_ref", "")
+
+
+def test_config_legs_parity_aggregation(monkeypatch):
+    """configs leg bookkeeping on the CPU (row functions stubbed): every row's parity and
+    the host rows' per-route parities are collected; one mismatch makes parity_all False
+    (bench.py then exits non-zero), a row that raises is reported and leaves parity_all
+    None unless a mismatch was also seen."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import config_legs as CL
+    monkeypatch.setattr(CL, "Timer", lambda TE: None)
+    monkeypatch.setattr(CL.torch.cuda, "empty_cache", lambda: None)
+    ok = {"match": True}
+    monkeypatch.setattr(CL, "c2", lambda W, T, D: {"config": "C2", "parity": ok})
+    monkeypatch.setattr(CL, "c5", lambda W, T, D, s, stream_kernel=False: {"config": "C5", "parity": ok})
+    monkeypatch.setattr(CL, "verify_and_build", lambda W, T, D: [{"config": "verify", "parity": ok}])
+    host = [{"config": "C3", "pinned": {"parity": ok}, "pageable": {"parity": ok}}]
+    monkeypatch.setattr(CL, "host_rows", lambda W, D: host)
+    r = CL.run(None, None)
+    assert r["parity_all"] is True and r["parity_checks"] == 7
+    host[0]["pageable"]["parity"] = {"match": False}
+    assert CL.run(None, None)["parity_all"] is False
+
+    def boom(W, D):
+        raise RuntimeError("no pinned memory")
+    monkeypatch.setattr(CL, "host_rows", boom)
+    r = CL.run(None, None)
+    assert r["parity_all"] is None and any("error" in x for x in r["rows"])
+    assert CL.run(None, None, only="c2")["parity_checks"] == 1
