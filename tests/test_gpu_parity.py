@@ -1708,3 +1708,71 @@ def test_fast_path_frame_placements(W, lead):
         out = u32_out(n)
         W.crc32_batch_fixed(d[lead:], stride, L, n, out)
         assert np.array_equal(to_u32(out, n), O.batch_fixed(host[lead:], stride, L, n)), (L, stride)
+
+
+# ---- size-independent properties at full config sizes -----------------------------------
+# CRC-32 is affine over GF(2): for equal-length messages x, y,
+#   crc(x ^ y) = crc(x) ^ crc(y) ^ crc(0^len).
+# Checked for EVERY packet at C4's per-rank size and for C5's distribution below and past
+# 2 GiB (device-only, so nothing is sampled), with crc(0^len) itself pinned to the oracle
+# for every length that occurs (1456 x 0x00 -> 0x16BCBC70 is a reference KAT).
+def _xor_pair(nbytes, seeds=(0x5EED, 0xC0FFEE)):
+    a = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+    b = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+    import wtp_crc32 as W
+    W.synth_fill(a, seed=seeds[0], nbytes=nbytes)
+    W.synth_fill(b, seed=seeds[1], nbytes=nbytes)
+    c = torch.bitwise_xor(a, b)
+    z = torch.zeros_like(a)
+    return a, b, c, z
+
+
+def test_linearity_c4_rank_shard_every_packet(W):
+    """C4's per-rank shard, 2,097,152 x 1456 B (3.05 GB; the held-results braided launch):
+    crc(A ^ B) == crc(A) ^ crc(B) ^ crc(0) for all 2 M packets, crc(0) == 0x16BCBC70."""
+    n = 2_097_152
+    bufs = _xor_pair(n * 1456)
+    outs = []
+    for t in bufs:
+        o = u32_out(n)
+        W.crc32_batch_fixed(t, 1456, 1456, n, o)
+        outs.append(o)
+    assert W.LIB.wtp_last_kernel().decode() == "k_fixed_braid<6, 0, CrcHoldBEpi>"
+    a, b, c, z = outs
+    assert torch.equal(torch.bitwise_xor(torch.bitwise_xor(a, b), z), c)
+    zu = to_u32(z, n)
+    assert (zu == np.uint32(0x16BCBC70)).all() and O.crc32(bytes(1456)) == 0x16BCBC70
+    assert not torch.equal(a, b)
+    del bufs
+
+
+@pytest.mark.parametrize("n", [1 << 20, 17_000_000])
+def test_linearity_zipf_packed_every_payload(W, n):
+    """C5's Zipf(1.1) lengths, packed: 1 M payloads (one piece launch) and 17 M (2.3 GB: the
+    device-cut sub-launches past 2 GiB).  Every payload: crc(A ^ B) == crc(A) ^ crc(B) ^
+    crc(0^len), and crc(0^len) equal to the oracle's for each distinct length."""
+    lens = O.zipf_lengths(n, s=1.1).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    bufs = _xor_pair(total)
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    outs = []
+    for t in bufs:
+        o = u32_out(n)
+        W.crc32_batch_packed(t, total, do, dl, n, o)
+        outs.append(o)
+    if total + 64 >= (1 << 31):
+        assert W.LIB.wtp_last_kernel().decode().startswith("k_pieces<RangeArrayProvL")
+    a, b, c, z = outs
+    assert torch.equal(torch.bitwise_xor(torch.bitwise_xor(a, b), z), c)
+    zu = to_u32(z, n)
+    for L in np.unique(lens):
+        first = int(np.argmax(lens == L))
+        assert int(zu[first]) == O.crc32(bytes(int(L))), L
+    # every payload of one length has the same crc(0^len)
+    order = np.argsort(lens, kind="stable")
+    ls, zs = lens[order], zu[order]
+    starts = np.concatenate([[True], ls[1:] != ls[:-1]])
+    assert np.array_equal(zs, np.repeat(zs[starts], np.diff(np.concatenate([np.nonzero(starts)[0], [n]]))))
+    del bufs
